@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark of the dense simplex pivot hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One "step" = one simplex pivot (entering scan, ratio test, rank-1 update of
+the whole float64 tableau) with the standard rule, all on the device.
+Workload (weak scaling): every GPU holds 4096 constraint rows
+of an 8192-variable tableau.
+  N = 1 : cfg3, G_mixed(m=4096, ns=4096, seed 3) -> a 4097 x 8193 tableau
+  N > 1 : G_tall(m=4096*N, n=8192, seed 3), rows sharded 4096 per rank
+          (N = 8 is cfg4, the 32768 x 8192 tableau); RCCL exchange per pivot.
+``value`` = pivots/s x N (each pivot sweeps N shards of 4096 x 8192), i.e.
+plain LP pivots/s at N = 1; ``lp_pivots_per_s`` is the LP-level rate.
+
+Inputs are resident in HBM before the timed region.  The rank-1 update
+kernel's launches inside the timed region are bracketed by HIP events on the
+engine's stream (lp_profile) for the roofline's achieved bandwidth.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from lpsol_amd import _lib  # noqa: E402
+from lpsol_amd import generators as gen  # noqa: E402
+
+METRIC = "pivots/sec + achieved HBM GB/s on dense float64 tableau, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+ROWS_PER_GPU = 4096
+NCOLS = 8192
+SEED = 3
+
+
+def pivot_bytes(m: int, n: int) -> int:
+    """Algorithmic bytes of one pivot: read+write the whole
+    tableau, the row-0 scan and the column+b ratio gather."""
+    return 8 * (2 * (m + 1) * (n + 1) + (n + 1) + 2 * (m + 1))
+
+
+def update_bytes(rows: int, n: int) -> int:
+    """Algorithmic bytes of one k_update launch on `rows` local rows: read and
+    write every row, read the pivot row P and the multiplier column."""
+    return 8 * (2 * rows * (n + 1) + (n + 1) + rows)
+
+
+def workload(nranks: int, rank: int):
+    """(kind, m, ns, n, row block) of this rank."""
+    if nranks == 1:
+        kind, m, ns = "mixed", ROWS_PER_GPU, NCOLS - ROWS_PER_GPU
+    else:
+        kind, m, ns = "tall", ROWS_PER_GPU * nranks, NCOLS
+    _, n = gen.shape(kind, m, ns)
+    rb = m * rank // nranks
+    re_ = m * (rank + 1) // nranks
+    return kind, m, ns, n, rb, re_
+
+
+def cpu_baseline(seconds_target: float = 15.0) -> dict:
+    """Exact-Fraction oracle (the reference's algorithm, oracle/exact.py) on
+    the first standard-rule pivot of cfg3, applied to a bounded row sample and
+    scaled to the full 4097-row tableau.  Single core."""
+    from oracle import exact
+    kind, m, ns = "mixed", ROWS_PER_GPU, NCOLS - ROWS_PER_GPU
+    T = gen.tableau(kind, m, ns, SEED)
+    # selection on the full tableau (cheap: row 0 + one column)
+    c = int(np.argmin(T[0, 1:]))
+    col = T[1:, 1 + c]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = np.where(col > 0, T[1:, 0] / np.where(col > 0, col, 1), np.inf)
+    r = int(np.argmin(q))
+    # sample: row 0, the pivot row and the first S other rows
+    t0 = time.perf_counter()
+    S, total, rows_done = 16, 0.0, 0
+    others = [i for i in range(m) if i != r]
+    while total < seconds_target and rows_done + S <= len(others):
+        pick = others[rows_done:rows_done + S]
+        sub = exact.from_array(np.vstack([T[:1], T[1 + r:2 + r], T[[1 + i for i in pick]]]))
+        t1 = time.perf_counter()
+        exact.pivot(sub, 0, c)
+        total += time.perf_counter() - t1
+        rows_done += S
+        S = min(2 * S, 256)
+        if time.perf_counter() - t0 > 3 * seconds_target:
+            break
+    # rows_done updated rows (+ one row 0 and one pivot row per chunk, ignored:
+    # conservative) -> seconds for the m + 1 rows of a full pivot
+    sec_per_pivot = total / rows_done * (m + 1)
+    return {"value": 1.0 / sec_per_pivot, "unit": "pivots/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/exact.py Fraction pivot #1 of cfg3 (G_mixed 4096x8192 seed 3) "
+                       f"on {rows_done} of 4097 rows ({total:.1f} s), scaled to all rows; "
+                       f"host has {os.cpu_count()} cores"),
+            "seconds_per_pivot": sec_per_pivot}
+
+
+def load_traffic(path: str | None):
+    if path and os.path.exists(path):
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01",
+                                                            "hbm_traffic.json"))
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="1-GPU diagnostic: run the N-rank job's whole tableau on one GPU")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
+        raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # plumbing only: uid exchange, barriers, max
+        dist.init_process_group("gloo")
+
+    nsim = args.emulate_ranks if args.emulate_ranks else world
+    kind, m, ns, n, rb, re_ = workload(nsim, rank if world > 1 else 0)
+    if world == 1:
+        rb, re_ = 0, m
+    if world > 1:
+        uid = _lib.comm_unique_id() if rank == 0 else None
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        eng = _lib.create_sharded(m, n, rank, world, box[0], device=local)
+        assert (eng.row_begin, eng.row_count) == (rb, re_ - rb)
+    else:
+        eng = _lib.Engine(m, n, device=local)
+    eng.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
+    blk = 2048
+    for a in range(rb, re_, blk):
+        b = min(a + blk, re_)
+        eng.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + b))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    st, done = eng.run(_lib.RULE_STANDARD, args.warmup)     # ends with a stream sync
+    if done != args.warmup:
+        raise SystemExit(f"warmup ended early: status {st} after {done} pivots")
+    barrier()
+    eng.profile(True)
+    t0 = time.perf_counter()
+    st, done = eng.run(_lib.RULE_STANDARD, args.steps)      # enqueue + final stream sync
+    t1 = time.perf_counter()
+    barrier()
+    if done != args.steps:
+        raise SystemExit(f"timed run ended early: status {st} after {done} pivots")
+    upd_ms, upd_n = eng.update_time()
+    eng.profile(False)
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed, upd_ms / max(upd_n, 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, upd_avg_ms = float(t[0]), float(t[1])
+    else:
+        upd_avg_ms = upd_ms / max(upd_n, 1)
+
+    lp_pps = args.steps / elapsed
+    local_rows = (re_ - rb) + 1
+    achieved = update_bytes(local_rows, n) / (upd_avg_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic_json) if world == 1 else None
+    out = {
+        "metric": METRIC,
+        "value": lp_pps * world,
+        "unit": "pivots/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (counter-based splitmix64 dyadic k/64 LP, lpsol_amd.generators)",
+        "config": {
+            "workload": ("cfg3: 4096x8192 float64 tableau, G_mixed seed 3" if world == 1 else
+                         f"G_tall {m}x{n} float64 tableau seed 3, {ROWS_PER_GPU} rows per GPU"
+                         + (" (cfg4)" if world == 8 else "")),
+            "m": m, "n": n, "rows_per_gpu": re_ - rb, "rule": "standard (findPivotStandard)",
+            "parallelism": f"row-shard x{world}" + (" over RCCL" if world > 1 else ""),
+        },
+        "lp_pivots_per_s": lp_pps,
+        "achieved_GBps": pivot_bytes(m, n) * lp_pps / 1e9,
+        "roofline": {
+            "kernel": "k_update (rank-1 elimination)",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "bytes_per_launch": update_bytes(local_rows, n),
+            "avg_launch_us": upd_avg_ms * 1e3,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

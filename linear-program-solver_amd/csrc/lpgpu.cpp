@@ -1,0 +1,706 @@
+// liblpgpu.so: host side of the C-ABI declared in include/lpgpu.h.
+//
+// Owns device memory, the HIP stream and the device-resident pivot loop.  A
+// pivot never round-trips to the host: the host enqueues batches of pivot
+// launches and reads only the control block back between batches.
+//
+// Row sharding: a handle may be one shard of a row-partitioned tableau.  The
+// shards exchange two messages per pivot through a Comm:
+//   allreduce-min of the local minimum ratio (8 B)   -> every rank knows g
+//   allgather of one slot per rank (header + row)    -> every rank knows the
+//                                                       leaving row and P
+// Comm has two transports: RCCL (one process per GPU, production) and an
+// in-process group of shards on one device (the test-suite uses it to prove
+// that the pivot sequence does not depend on the shard count).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+using lpk::Args;
+using lpk::Ctl;
+using lpk::Rec;
+
+struct Comm;
+
+struct lp_handle {
+    int dev = 0;
+    hipStream_t s = nullptr;
+    bool own_stream = true;
+    int64_t m = 0, n = 0, ld = 0;   // global problem
+    int64_t rb = 0, rc = 0;         // local constraint block [rb, rb+rc)
+    int64_t rows = 0;               // local rows = rc + 1
+    double *T = nullptr, *P = nullptr, *mult = nullptr;
+    Ctl *ctl = nullptr;
+    Ctl *hctl = nullptr;            // pinned mirror
+    long long *log = nullptr;
+    int64_t logcap = 0;
+    Rec *rec = nullptr;
+    double *xg = nullptr, *xs = nullptr, *xr = nullptr;   // sharded exchange buffers
+    lp_tol tol{};
+    bool prof = false;
+    std::vector<hipEvent_t> ev;     // pairs (start, end) of update launches
+    size_t evused = 0;
+    double prof_ms = 0.0;
+    int64_t prof_n = 0;
+    int rank = 0, nranks = 1;
+    std::shared_ptr<Comm> comm;     // null: single device, no exchange
+    std::string err;
+};
+
+static std::string g_create_err;
+
+#define HCHK(h, expr)                                                              \
+    do {                                                                           \
+        hipError_t e_ = (expr);                                                    \
+        if (e_ != hipSuccess) {                                                    \
+            (h)->err = std::string(#expr) + ": " + hipGetErrorString(e_);          \
+            return LP_DEVICE_ERROR;                                                \
+        }                                                                          \
+    } while (0)
+
+#define NCHK(h, expr)                                                              \
+    do {                                                                           \
+        ncclResult_t e_ = (expr);                                                  \
+        if (e_ != ncclSuccess) {                                                   \
+            (h)->err = std::string(#expr) + ": " + ncclGetErrorString(e_);         \
+            return LP_DEVICE_ERROR;                                                \
+        }                                                                          \
+    } while (0)
+
+#define CALL(expr)                                                                 \
+    do {                                                                           \
+        const int st_ = (expr);                                                    \
+        if (st_ != LP_PIVOTED) return st_;                                         \
+    } while (0)
+
+static int fail(lp_handle *h, int code, const std::string &msg)
+{
+    h->err = msg;
+    return code;
+}
+
+static int64_t slot_len(const lp_handle *h) { return lpk::SLOT_HDR + h->ld; }
+
+// ---------------------------------------------------------------------------
+// transports
+// ---------------------------------------------------------------------------
+
+using Members = std::vector<lp_handle *>;
+
+struct Comm {
+    virtual ~Comm() {}
+    // the handles whose pivot loops this process drives in lock-step
+    virtual Members members(lp_handle *h) = 0;
+    virtual int allreduce_min(const Members &M) = 0;   // xg, one double, in place
+    virtual int allgather(const Members &M) = 0;       // xs -> xr
+};
+
+struct RcclComm : Comm {
+    ncclComm_t comm = nullptr;
+    ~RcclComm() override
+    {
+        if (comm) ncclCommDestroy(comm);
+    }
+    Members members(lp_handle *h) override { return Members{h}; }
+    int allreduce_min(const Members &M) override
+    {
+        lp_handle *h = M[0];
+        NCHK(h, ncclAllReduce(h->xg, h->xg, 1, ncclFloat64, ncclMin, comm, h->s));
+        return LP_PIVOTED;
+    }
+    int allgather(const Members &M) override
+    {
+        lp_handle *h = M[0];
+        NCHK(h, ncclAllGather(h->xs, h->xr, (size_t)slot_len(h), ncclFloat64, comm, h->s));
+        return LP_PIVOTED;
+    }
+};
+
+struct GroupComm : Comm {
+    Members all;                   // every shard, rank order
+    double **dptrs = nullptr;      // device array of the shards' xg pointers
+    hipStream_t s = nullptr;       // shared by all shards, released with the last one
+    ~GroupComm() override
+    {
+        if (dptrs) (void)hipFree(dptrs);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    Members members(lp_handle *) override { return all; }
+    int allreduce_min(const Members &M) override
+    {
+        lp_handle *h = M[0];
+        HCHK(h, lpk::launch_group_min(h->s, dptrs, (int)M.size()));
+        return LP_PIVOTED;
+    }
+    int allgather(const Members &M) override
+    {
+        const size_t bytes = (size_t)slot_len(M[0]) * sizeof(double);
+        for (lp_handle *dst : M)
+            for (size_t k = 0; k < M.size(); ++k)
+                HCHK(dst, hipMemcpyAsync(dst->xr + k * slot_len(dst), M[k]->xs, bytes,
+                                         hipMemcpyDeviceToDevice, dst->s));
+        return LP_PIVOTED;
+    }
+};
+
+static Members members_of(lp_handle *h) { return h->comm ? h->comm->members(h) : Members{h}; }
+
+// ---------------------------------------------------------------------------
+// creation
+// ---------------------------------------------------------------------------
+
+static Args args_of(const lp_handle *h)
+{
+    Args A;
+    A.T = h->T;
+    A.P = h->P;
+    A.mult = h->mult;
+    A.ctl = h->ctl;
+    A.log = h->log;
+    A.rec = h->rec;
+    A.xg = h->xg;
+    A.xs = h->xs;
+    A.xr = h->xr;
+    A.logcap = h->logcap;
+    A.m = h->m;
+    A.n = h->n;
+    A.ld = h->ld;
+    A.rows = h->rows;
+    A.rb = h->rb;
+    A.rc = h->rc;
+    A.nranks = h->nranks;
+    A.pad = 0;
+    A.tol = h->tol;
+    return A;
+}
+
+extern "C" void lp_default_tol(lp_tol *t)
+{
+    t->cost = 1e-9;
+    t->cost_tie = 1e-12;
+    t->pivot = 1e-9;
+    t->zero = 1e-9;
+    t->ratio_tie = 1e-12;
+    t->stall = 1e-12;
+}
+
+extern "C" int lp_device_count(int *count)
+{
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return LP_PIVOTED;
+}
+
+static void init_geometry(lp_handle *h, int64_t m, int64_t n, int rank, int nranks)
+{
+    h->m = m;
+    h->n = n;
+    h->ld = (n + 1 + 63) / 64 * 64;
+    h->rank = rank;
+    h->nranks = nranks;
+    h->rb = m * rank / nranks;
+    h->rc = m * (rank + 1) / nranks - h->rb;
+    h->rows = h->rc + 1;
+}
+
+static int alloc_handle(lp_handle *h)
+{
+    HCHK(h, hipSetDevice(h->dev));
+    if (!h->s) HCHK(h, hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
+    const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
+    HCHK(h, hipMalloc(&h->T, tbytes));
+    HCHK(h, hipMemsetAsync(h->T, 0, tbytes, h->s));
+    HCHK(h, hipMalloc(&h->P, (size_t)h->ld * sizeof(double)));
+    HCHK(h, hipMemsetAsync(h->P, 0, (size_t)h->ld * sizeof(double), h->s));
+    HCHK(h, hipMalloc(&h->mult, (size_t)h->rows * sizeof(double)));
+    HCHK(h, hipMalloc(&h->ctl, sizeof(Ctl)));
+    HCHK(h, hipMemsetAsync(h->ctl, 0, sizeof(Ctl), h->s));
+    HCHK(h, hipHostMalloc(&h->hctl, sizeof(Ctl), hipHostMallocDefault));
+    std::memset(h->hctl, 0, sizeof(Ctl));
+    h->logcap = 4096;
+    HCHK(h, hipMalloc(&h->log, (size_t)h->logcap * 2 * sizeof(long long)));
+    const int nrec = std::max(1, lpk::ratio_blocks(h->rows));
+    HCHK(h, hipMalloc(&h->rec, (size_t)nrec * sizeof(Rec)));
+    if (h->nranks > 1 || h->comm) {
+        HCHK(h, hipMalloc(&h->xg, sizeof(double)));
+        HCHK(h, hipMalloc(&h->xs, (size_t)slot_len(h) * sizeof(double)));
+        HCHK(h, hipMalloc(&h->xr, (size_t)slot_len(h) * h->nranks * sizeof(double)));
+        HCHK(h, hipMemsetAsync(h->xs, 0, (size_t)slot_len(h) * sizeof(double), h->s));
+    }
+    HCHK(h, hipStreamSynchronize(h->s));
+    lp_default_tol(&h->tol);
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_create(int64_t m, int64_t n, int device, lp_handle **out)
+{
+    *out = nullptr;
+    if (m <= 0 || n <= 0) {
+        g_create_err = "need m > 0 and n > 0";
+        return LP_BAD_ARG;
+    }
+    lp_handle *h = new lp_handle;
+    h->dev = device;
+    init_geometry(h, m, n, 0, 1);
+    const int st = alloc_handle(h);
+    if (st != LP_PIVOTED) {
+        g_create_err = h->err;
+        lp_destroy(h);
+        return st;
+    }
+    *out = h;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_comm_unique_id(void *uid128)
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        g_create_err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return LP_DEVICE_ERROR;
+    }
+    std::memcpy(uid128, &id, sizeof(id));
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_create_sharded(int64_t m, int64_t n, int device, int rank, int nranks,
+                                 const void *uid128, lp_handle **out)
+{
+    *out = nullptr;
+    if (m <= 0 || n <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || m < nranks) {
+        g_create_err = "need m >= nranks > 0, n > 0 and 0 <= rank < nranks";
+        return LP_BAD_ARG;
+    }
+    lp_handle *h = new lp_handle;
+    h->dev = device;
+    init_geometry(h, m, n, rank, nranks);
+    auto comm = std::make_shared<RcclComm>();
+    h->comm = comm;
+    int st = alloc_handle(h);
+    if (st == LP_PIVOTED) {
+        ncclUniqueId id;
+        std::memcpy(&id, uid128, sizeof(id));
+        const ncclResult_t r = ncclCommInitRank(&comm->comm, nranks, id, rank);
+        if (r != ncclSuccess) {
+            h->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            st = LP_DEVICE_ERROR;
+        }
+    }
+    if (st != LP_PIVOTED) {
+        g_create_err = h->err;
+        lp_destroy(h);
+        return st;
+    }
+    *out = h;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_create_group(int64_t m, int64_t n, int device, int nshards, lp_handle **out)
+{
+    for (int k = 0; k < nshards; ++k) out[k] = nullptr;
+    if (m <= 0 || n <= 0 || nshards <= 0 || m < nshards) {
+        g_create_err = "need m >= nshards > 0 and n > 0";
+        return LP_BAD_ARG;
+    }
+    auto grp = std::make_shared<GroupComm>();
+    hipStream_t s = nullptr;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        g_create_err = "stream creation failed";
+        return LP_DEVICE_ERROR;
+    }
+    grp->s = s;
+    int st = LP_PIVOTED;
+    for (int k = 0; k < nshards && st == LP_PIVOTED; ++k) {
+        lp_handle *h = new lp_handle;
+        h->dev = device;
+        h->s = s;
+        h->own_stream = false;
+        init_geometry(h, m, n, k, nshards);
+        h->comm = grp;
+        grp->all.push_back(h);
+        out[k] = h;
+        st = alloc_handle(h);
+        if (st != LP_PIVOTED) g_create_err = h->err;
+    }
+    if (st == LP_PIVOTED) {
+        std::vector<double *> p;
+        for (lp_handle *h : grp->all) p.push_back(h->xg);
+        if (hipMalloc(&grp->dptrs, p.size() * sizeof(double *)) != hipSuccess ||
+            hipMemcpy(grp->dptrs, p.data(), p.size() * sizeof(double *), hipMemcpyHostToDevice) !=
+                hipSuccess) {
+            g_create_err = "group pointer table";
+            st = LP_DEVICE_ERROR;
+        }
+    }
+    if (st != LP_PIVOTED) {
+        for (int k = nshards - 1; k >= 0; --k)
+            if (out[k]) {
+                lp_destroy(out[k]);
+                out[k] = nullptr;
+            }
+        return st;
+    }
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_shard_rows(const lp_handle *h, int64_t *row_begin, int64_t *row_count)
+{
+    *row_begin = h->rb;
+    *row_count = h->rc;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_destroy(lp_handle *h)
+{
+    if (!h) return LP_PIVOTED;
+    (void)hipSetDevice(h->dev);
+    if (h->s) (void)hipStreamSynchronize(h->s);
+    for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->T) (void)hipFree(h->T);
+    if (h->P) (void)hipFree(h->P);
+    if (h->mult) (void)hipFree(h->mult);
+    if (h->ctl) (void)hipFree(h->ctl);
+    if (h->hctl) (void)hipHostFree(h->hctl);
+    if (h->log) (void)hipFree(h->log);
+    if (h->rec) (void)hipFree(h->rec);
+    if (h->xg) (void)hipFree(h->xg);
+    if (h->xs) (void)hipFree(h->xs);
+    if (h->xr) (void)hipFree(h->xr);
+    if (h->comm) {
+        if (auto g = std::dynamic_pointer_cast<GroupComm>(h->comm)) {
+            auto it = std::find(g->all.begin(), g->all.end(), h);
+            if (it != g->all.end()) *it = nullptr;
+        }
+        h->comm.reset();
+    }
+    if (h->s && h->own_stream) (void)hipStreamDestroy(h->s);
+    delete h;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_set_tol(lp_handle *h, const lp_tol *tol)
+{
+    for (lp_handle *x : members_of(h))
+        if (x) x->tol = *tol;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_get_tol(const lp_handle *h, lp_tol *tol)
+{
+    *tol = h->tol;
+    return LP_PIVOTED;
+}
+
+extern "C" const char *lp_last_error(const lp_handle *h)
+{
+    return h ? h->err.c_str() : g_create_err.c_str();
+}
+
+// ---------------------------------------------------------------------------
+// row transfers
+// ---------------------------------------------------------------------------
+
+// global row -> local row, or -1 if this rank does not hold it
+static int64_t local_row(const lp_handle *h, int64_t R)
+{
+    if (R == 0) return 0;
+    if (R >= 1 + h->rb && R < 1 + h->rb + h->rc) return R - h->rb;
+    return -1;
+}
+
+template <bool UP>
+static int transfer_rows(lp_handle *h, int64_t row0, int64_t nrows, double *buf, int64_t ldh)
+{
+    if (row0 < 0 || nrows < 0 || row0 + nrows > h->m + 1 || ldh < h->n + 1)
+        return fail(h, LP_BAD_ARG, "row range or leading dimension out of bounds");
+    HCHK(h, hipSetDevice(h->dev));
+    int64_t k = 0;
+    while (k < nrows) {
+        const int64_t R = row0 + k;
+        const int64_t L = local_row(h, R);
+        if (L < 0) return fail(h, LP_BAD_ARG, "row not held by this shard");
+        int64_t run = 1;   // longest run of consecutive local rows
+        if (R > 0)
+            while (k + run < nrows && local_row(h, R + run) == L + run) ++run;
+        double *dev = h->T + L * h->ld;
+        double *host = buf + k * ldh;
+        const size_t w = (size_t)(h->n + 1) * sizeof(double);
+        if (UP)
+            HCHK(h, hipMemcpy2DAsync(dev, h->ld * sizeof(double), host, ldh * sizeof(double), w,
+                                     run, hipMemcpyHostToDevice, h->s));
+        else
+            HCHK(h, hipMemcpy2DAsync(host, ldh * sizeof(double), dev, h->ld * sizeof(double), w,
+                                     run, hipMemcpyDeviceToHost, h->s));
+        k += run;
+    }
+    HCHK(h, hipStreamSynchronize(h->s));
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_upload_rows(lp_handle *h, int64_t row0, int64_t nrows, const double *src,
+                              int64_t ldh)
+{
+    return transfer_rows<true>(h, row0, nrows, const_cast<double *>(src), ldh);
+}
+
+extern "C" int lp_download_rows(lp_handle *h, int64_t row0, int64_t nrows, double *dst,
+                                int64_t ldh)
+{
+    return transfer_rows<false>(h, row0, nrows, dst, ldh);
+}
+
+// ---------------------------------------------------------------------------
+// pivot machinery
+// ---------------------------------------------------------------------------
+
+static int ensure_log(lp_handle *h, int64_t need)
+{
+    if (need <= h->logcap) return LP_PIVOTED;
+    int64_t cap = h->logcap;
+    while (cap < need) cap *= 2;
+    long long *nl = nullptr;
+    HCHK(h, hipMalloc(&nl, (size_t)cap * 2 * sizeof(long long)));
+    HCHK(h, hipMemcpyAsync(nl, h->log, (size_t)h->logcap * 2 * sizeof(long long),
+                           hipMemcpyDeviceToDevice, h->s));
+    HCHK(h, hipStreamSynchronize(h->s));
+    HCHK(h, hipFree(h->log));
+    h->log = nl;
+    h->logcap = cap;
+    return LP_PIVOTED;
+}
+
+static int launch_update_timed(lp_handle *h, const Args &A)
+{
+    if (!h->prof) {
+        HCHK(h, lpk::launch_update(h->s, A));
+        return LP_PIVOTED;
+    }
+    if (h->evused + 2 > h->ev.size()) {
+        hipEvent_t a, b;
+        HCHK(h, hipEventCreate(&a));
+        HCHK(h, hipEventCreate(&b));
+        h->ev.push_back(a);
+        h->ev.push_back(b);
+    }
+    HCHK(h, hipEventRecord(h->ev[h->evused], h->s));
+    HCHK(h, lpk::launch_update(h->s, A));
+    HCHK(h, hipEventRecord(h->ev[h->evused + 1], h->s));
+    h->evused += 2;
+    return LP_PIVOTED;
+}
+
+// after a stream sync: fold recorded update launches into the totals
+static int collect_profile(lp_handle *h)
+{
+    for (size_t k = 0; k + 1 < h->evused; k += 2) {
+        float ms = 0.f;
+        HCHK(h, hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
+        h->prof_ms += ms;
+        h->prof_n += 1;
+    }
+    h->evused = 0;
+    return LP_PIVOTED;
+}
+
+static int sync_ctl(const Members &M)
+{
+    for (lp_handle *h : M) {
+        HCHK(h, hipSetDevice(h->dev));
+        HCHK(h, hipMemcpyAsync(h->hctl, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+    }
+    for (lp_handle *h : M) {
+        HCHK(h, hipStreamSynchronize(h->s));
+        CALL(collect_profile(h));
+    }
+    return LP_PIVOTED;
+}
+
+static std::vector<Args> args_all(const Members &M)
+{
+    std::vector<Args> v;
+    for (lp_handle *h : M) v.push_back(args_of(h));
+    return v;
+}
+
+// Everything after the entering scan of one pivot.  sel: 0 = ratio test,
+// 1 = validated row (Simplex.pivot), 2 = explicit row (Tableau.pivot).
+// do_update=false stops after the pivot row is known (findPivot*(False)).
+static int enqueue_tail(const Members &M, const std::vector<Args> &A, int sel, bool do_update)
+{
+    lp_handle *h0 = M[0];
+    if (!h0->comm) {
+        if (sel == 0) HCHK(h0, lpk::launch_ratio(h0->s, A[0], lpk::RATIO_FULL, -1));
+        else if (sel == 1)
+            HCHK(h0, lpk::launch_ratio(h0->s, A[0], lpk::RATIO_CHECK,
+                                       local_row(h0, h0->hctl->r + 1)));
+        else HCHK(h0, lpk::launch_gather(h0->s, A[0]));
+        if (!do_update) return LP_PIVOTED;
+        HCHK(h0, lpk::launch_prow(h0->s, A[0]));
+        return launch_update_timed(h0, A[0]);
+    }
+    for (size_t k = 0; k < M.size(); ++k) {
+        if (sel == 2) HCHK(M[k], lpk::launch_gather(M[k]->s, A[k]));
+        else HCHK(M[k], lpk::launch_ratio(M[k]->s, A[k], lpk::RATIO_LOCAL, -1));
+    }
+    if (sel != 2) CALL(h0->comm->allreduce_min(M));
+    const int pm = sel == 0 ? lpk::PICK_RATIO : sel == 1 ? lpk::PICK_CHECK : lpk::PICK_EXPLICIT;
+    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_pick(M[k]->s, A[k], pm));
+    CALL(h0->comm->allgather(M));
+    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_prow_sharded(M[k]->s, A[k]));
+    if (!do_update) return LP_PIVOTED;
+    for (size_t k = 0; k < M.size(); ++k) CALL(launch_update_timed(M[k], A[k]));
+    return LP_PIVOTED;
+}
+
+static int enqueue_pivot(const Members &M, const std::vector<Args> &A)
+{
+    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
+    return enqueue_tail(M, A, 0, true);
+}
+
+static int reset_all(const Members &M, int mode, int rule, int64_t cap, int64_t r, int64_t c)
+{
+    for (lp_handle *h : M) {
+        HCHK(h, hipSetDevice(h->dev));
+        HCHK(h, lpk::launch_reset(h->s, h->ctl, mode, rule, cap, r, c, h->T));
+        h->hctl->r = r;
+        h->hctl->c = c;
+    }
+    return LP_PIVOTED;
+}
+
+// Runs pivots until the device reports a status other than LP_PIVOTED or
+// `limit` pivots have been enqueued (limit < 0: unlimited).  Batch sizes are
+// a deterministic sequence, so every rank of a sharded job enqueues the same
+// collectives in the same order.
+static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t limit)
+{
+    const Members M = members_of(h);
+    CALL(reset_all(M, mode, rule, cap, -1, -1));
+    int64_t enq = 0;
+    int64_t batch = 8;
+    for (;;) {
+        int64_t b = batch;
+        if (limit >= 0) b = std::min(b, limit - enq);
+        for (lp_handle *x : M) CALL(ensure_log(x, enq + b));
+        const std::vector<Args> A = args_all(M);
+        for (int64_t k = 0; k < b; ++k) CALL(enqueue_pivot(M, A));
+        enq += b;
+        CALL(sync_ctl(M));
+        if (h->hctl->status != LP_PIVOTED) return h->hctl->status;
+        if (limit >= 0 && enq >= limit) return LP_PIVOTED;
+        batch = std::min<int64_t>(batch * 2, 1024);
+    }
+}
+
+extern "C" int lp_solve(lp_handle *h, int64_t max_pivots, int64_t *npiv, int64_t *nstd)
+{
+    const int st = pivot_loop(h, lpk::MODE_SOLVE, LP_RULE_STANDARD, max_pivots, -1);
+    *npiv = h->hctl->npiv;
+    *nstd = h->hctl->nstd;
+    return st;
+}
+
+extern "C" int lp_run(lp_handle *h, int rule, int64_t k, int64_t *done)
+{
+    *done = 0;
+    if (rule != LP_RULE_STANDARD && rule != LP_RULE_MIN_INDEX)
+        return fail(h, LP_BAD_ARG, "unknown rule");
+    if (k < 0) return fail(h, LP_BAD_ARG, "k < 0");
+    const int st = pivot_loop(h, lpk::MODE_RUN, rule, -1, k);
+    *done = h->hctl->npiv;
+    return st;
+}
+
+extern "C" int lp_find_pivot(lp_handle *h, int rule, int do_pivot, int64_t *r, int64_t *c)
+{
+    *r = -1;
+    *c = -1;
+    if (rule != LP_RULE_STANDARD && rule != LP_RULE_MIN_INDEX)
+        return fail(h, LP_BAD_ARG, "unknown rule");
+    const Members M = members_of(h);
+    CALL(reset_all(M, lpk::MODE_RUN, rule, -1, -1, -1));
+    const std::vector<Args> A = args_all(M);
+    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
+    CALL(enqueue_tail(M, A, 0, do_pivot != 0));
+    CALL(sync_ctl(M));
+    if (h->hctl->status == LP_PIVOTED) {
+        *r = h->hctl->r;
+        *c = h->hctl->c;
+    }
+    return h->hctl->status;
+}
+
+static int explicit_pivot(lp_handle *h, int64_t r, int64_t c, bool checked)
+{
+    if (r < 0 || r >= h->m || c < 0 || c >= h->n)
+        return fail(h, LP_BAD_ARG, "pivot index out of range");
+    const Members M = members_of(h);
+    CALL(reset_all(M, lpk::MODE_RUN, LP_RULE_STANDARD, -1, r, c));
+    const std::vector<Args> A = args_all(M);
+    CALL(enqueue_tail(M, A, checked ? 1 : 2, true));
+    CALL(sync_ctl(M));
+    return h->hctl->status;
+}
+
+extern "C" int lp_pivot(lp_handle *h, int64_t r, int64_t c) { return explicit_pivot(h, r, c, false); }
+
+extern "C" int lp_pivot_checked(lp_handle *h, int64_t r, int64_t c)
+{
+    return explicit_pivot(h, r, c, true);
+}
+
+extern "C" int lp_pivot_log(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count)
+{
+    const int64_t n = h->hctl->npiv;
+    *count = n;
+    const int64_t k = std::min(std::min(n, cap), h->logcap);
+    if (k > 0) {
+        HCHK(h, hipSetDevice(h->dev));
+        HCHK(h, hipMemcpyAsync(rc, h->log, (size_t)k * 2 * sizeof(long long),
+                               hipMemcpyDeviceToHost, h->s));
+        HCHK(h, hipStreamSynchronize(h->s));
+    }
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_objective(lp_handle *h, double *z)
+{
+    double v = 0.0;
+    HCHK(h, hipSetDevice(h->dev));
+    HCHK(h, hipMemcpyAsync(&v, h->T, sizeof(double), hipMemcpyDeviceToHost, h->s));
+    HCHK(h, hipStreamSynchronize(h->s));
+    *z = -v;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_profile(lp_handle *h, int enable)
+{
+    for (lp_handle *x : members_of(h)) {
+        if (!x) continue;
+        x->prof = enable != 0;
+        x->prof_ms = 0.0;
+        x->prof_n = 0;
+        x->evused = 0;
+    }
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_update_time(lp_handle *h, double *ms, int64_t *launches)
+{
+    *ms = h->prof_ms;
+    *launches = h->prof_n;
+    return LP_PIVOTED;
+}

@@ -1,0 +1,160 @@
+/*
+ * ORACLE -- test infrastructure only, never part of the product path.
+ *
+ * Scalar float64 restatement of the reference's dense simplex hot path with
+ * EXACTLY the floating-point semantics the HIP engine implements, so the
+ * engine's whole tableau can be compared BIT FOR BIT at sizes where the
+ * exact-Fraction oracle (oracle/exact.py) is too slow.  Its own agreement
+ * with the reference (pivot sequences, objectives) is pinned by the golden
+ * vectors in tests/golden/ (tests/test_oracle.py).
+ *
+ * Reference being restated (tkoz0/linear-program-solver, package lpsol):
+ *   lpf_pivot      <- Tableau.pivot            lpsol/tableau.py:295-308
+ *   lpf_find (0)   <- findPivotStandard        lpsol/simplex.py:251-284
+ *   lpf_find (1)   <- findPivotMinIndex        lpsol/simplex.py:218-249
+ *   lpf_solve      <- Simplex.solve            lpsol/simplex.py:110-148
+ *
+ * Float semantics (the contract shared with linear-program-solver_amd/csrc):
+ *   pivot(r,c): R=r+1, C=c+1, a=T[R][C] (a==0 -> ZERO_PIVOT)
+ *     P[j] = T[R][j] / a (IEEE division), P[C] = 1
+ *     for every row i != R with f = T[i][C] != 0:
+ *         T[i][j] = fma(-f, P[j], T[i][j])  for j != C,   T[i][C] = 0
+ *     T[R] = P
+ *   entering, standard : g = min c_j; optimal unless g < -tol.cost;
+ *                        c = first j with c_j <= g + tol.cost_tie*|g|
+ *   entering, min-index: c = first j with c_j < -tol.cost
+ *   ratio test         : rows with a_ic > tol.pivot; num = |b_i| <= tol.zero ? 0 : b_i
+ *                        q_i = num / a_ic; g = min q; r = first i with
+ *                        q_i <= g + tol.ratio_tie*|g|
+ *   stall (solve)      : |z - z0| <= tol.stall * max(1, |z0|)
+ * Build with -ffp-contract=off (no implicit fusing anywhere).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/lpgpu.h"
+
+static double *row(double *T, int64_t ld, int64_t i) { return T + i * ld; }
+
+int lpf_pivot(double *T, int64_t m, int64_t n, int64_t ld, int64_t r, int64_t c)
+{
+    if (r < 0 || r >= m || c < 0 || c >= n) return LP_BAD_ARG;
+    const int64_t R = r + 1, C = c + 1;
+    double *p = row(T, ld, R);
+    const double a = p[C];
+    if (a == 0.0) return LP_ZERO_PIVOT;
+    for (int64_t j = 0; j <= n; ++j) p[j] = p[j] / a;
+    p[C] = 1.0;
+    for (int64_t i = 0; i <= m; ++i) {
+        if (i == R) continue;
+        double *t = row(T, ld, i);
+        const double f = t[C];
+        if (f == 0.0) continue;
+        for (int64_t j = 0; j <= n; ++j) t[j] = fma(-f, p[j], t[j]);
+        t[C] = 0.0;
+    }
+    return LP_PIVOTED;
+}
+
+static int64_t entering(const double *T, int64_t n, int rule, const lp_tol *tol)
+{
+    const double *c0 = T;
+    if (rule == LP_RULE_MIN_INDEX) {
+        for (int64_t j = 1; j <= n; ++j)
+            if (c0[j] < -tol->cost) return j - 1;
+        return -1;
+    }
+    double g = INFINITY;
+    for (int64_t j = 1; j <= n; ++j)
+        if (c0[j] < g) g = c0[j];
+    if (!(g < -tol->cost)) return -1;
+    const double thr = g + tol->cost_tie * fabs(g);
+    for (int64_t j = 1; j <= n; ++j)
+        if (c0[j] <= thr) return j - 1;
+    return -1; /* unreachable */
+}
+
+static double ratio_of(const double *t, int64_t C, const lp_tol *tol, int *ok)
+{
+    const double a = t[C];
+    if (!(a > tol->pivot)) { *ok = 0; return 0.0; }
+    *ok = 1;
+    const double b = t[0];
+    const double num = fabs(b) <= tol->zero ? 0.0 : b;
+    return num / a;
+}
+
+static int64_t leaving(const double *T, int64_t m, int64_t ld, int64_t c, const lp_tol *tol)
+{
+    const int64_t C = c + 1;
+    double g = INFINITY;
+    int any = 0;
+    for (int64_t i = 1; i <= m; ++i) {
+        int ok;
+        const double q = ratio_of(T + i * ld, C, tol, &ok);
+        if (ok && (!any || q < g)) { g = q; any = 1; }
+    }
+    if (!any) return -1;
+    const double thr = g + tol->ratio_tie * fabs(g);
+    for (int64_t i = 1; i <= m; ++i) {
+        int ok;
+        const double q = ratio_of(T + i * ld, C, tol, &ok);
+        if (ok && q <= thr) return i - 1;
+    }
+    return -1; /* unreachable */
+}
+
+int lpf_find(const double *T, int64_t m, int64_t n, int64_t ld, int rule,
+             const lp_tol *tol, int64_t *r, int64_t *c)
+{
+    *r = -1;
+    *c = entering(T, n, rule, tol);
+    if (*c < 0) return LP_OPTIMAL;
+    *r = leaving(T, m, ld, *c, tol);
+    if (*r < 0) return LP_UNBOUNDED;
+    return LP_PIVOTED;
+}
+
+/* k pivots with one fixed rule (no stall logic); log gets 2 entries per pivot */
+int lpf_run(double *T, int64_t m, int64_t n, int64_t ld, int rule, const lp_tol *tol,
+            int64_t k, int64_t *log, int64_t *npiv)
+{
+    *npiv = 0;
+    for (int64_t t = 0; t < k; ++t) {
+        int64_t r, c;
+        const int st = lpf_find(T, m, n, ld, rule, tol, &r, &c);
+        if (st != LP_PIVOTED) return st;
+        lpf_pivot(T, m, n, ld, r, c);
+        if (log) { log[2 * t] = r; log[2 * t + 1] = c; }
+        ++*npiv;
+    }
+    return LP_PIVOTED;
+}
+
+int lpf_solve(double *T, int64_t m, int64_t n, int64_t ld, const lp_tol *tol,
+              int64_t cap, int64_t *log, int64_t *npiv, int64_t *nstd)
+{
+    *npiv = 0;
+    *nstd = 0;
+    const double z0 = -T[0];
+    int64_t stuck = 0;
+    int rule = LP_RULE_STANDARD;
+    for (;;) {
+        if (rule == LP_RULE_STANDARD && stuck >= m + n) rule = LP_RULE_MIN_INDEX;
+        if (cap >= 0 && *npiv >= cap) return LP_CAP_REACHED;
+        int64_t r, c;
+        const int st = lpf_find(T, m, n, ld, rule, tol, &r, &c);
+        if (st != LP_PIVOTED) return st;
+        lpf_pivot(T, m, n, ld, r, c);
+        if (log) { log[2 * *npiv] = r; log[2 * *npiv + 1] = c; }
+        ++*npiv;
+        if (rule == LP_RULE_STANDARD) {
+            ++*nstd;
+            const double z = -T[0];
+            if (fabs(z - z0) <= tol->stall * fmax(1.0, fabs(z0))) ++stuck;
+            else stuck = 0;
+        }
+    }
+}

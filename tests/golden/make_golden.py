@@ -1,0 +1,288 @@
+"""Capture golden vectors from the REFERENCE (tkoz0/linear-program-solver,
+package ``lpsol``) in the build container.
+
+Run from the repo root (needs /root/reference, read-only):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--big]
+
+It imports the reference, drives its own ``Tableau``/``Simplex`` on inputs
+from this repo's generator (``lpsol_amd.generators``) or on hand-built LPs,
+and records what the reference did: every ``Simplex._pivot(r, c)`` call in
+order, how many were standard-rule pivots, the final exact objective as
+``p/q`` and the final basic sequence.  Nothing of the reference's source is
+stored -- only inputs (as generator specs + sha256, or exact values for
+hand-built LPs) and outputs.  ``--big`` adds the slow cfg2 fixtures
+(512 x 1024, about 1-3 minutes each on one core).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from fractions import Fraction
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, "/root/reference")
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+
+from lpsol import Simplex, Tableau  # noqa: E402  (the reference)
+from lpsol_amd import generators as gen  # noqa: E402
+from oracle import exact  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def fs(x: Fraction) -> str:
+    return f"{x.numerator}/{x.denominator}"
+
+
+# ---------------------------------------------------------------- reference io
+
+def ref_tableau_from_rows(rows) -> Tableau:
+    """rows: exact Fractions in the engine layout (row 0 = [_z, c...])."""
+    m, n = len(rows) - 1, len(rows[0]) - 1
+    t = Tableau(m, n)
+    t.setZ(-rows[0][0])                     # setZ stores -z (tableau.py:128-130)
+    t.setC(rows[0][1:])
+    t.setB([rows[i][0] for i in range(1, m + 1)])
+    t.setA([rows[i][1:] for i in range(1, m + 1)])
+    t.setVarNames([f"x{j}" for j in range(n)])
+    return t
+
+
+def ref_rows(t: Tableau):
+    m, n = t.getTableauSize()
+    rows = [[-t.getZ()] + list(t.getC())]
+    for i in range(m):
+        rows.append([t.getBi(i)] + list(t.getA()[i]))
+    return rows
+
+
+class LoggingSimplex(Simplex):
+    """Reference Simplex that records each pivot and which rule chose it."""
+
+    def __init__(self, tab, log):
+        self._log = log
+        self._rule = "init"
+        super().__init__(tab)
+
+    def _pivot(self, r, c):
+        self._log.append((r, c, self._rule))
+        super()._pivot(r, c)
+
+    def findPivotStandard(self, do_pivot=False):
+        self._rule = "std"
+        return super().findPivotStandard(do_pivot)
+
+    def findPivotMinIndex(self, do_pivot=False):
+        self._rule = "min"
+        return super().findPivotMinIndex(do_pivot)
+
+
+def bare_simplex(tab, log):
+    """Simplex without phase 1 (harness-only bypass)."""
+    s = LoggingSimplex.__new__(LoggingSimplex)
+    s._log = log
+    s._rule = "init"
+    s._tab = tab
+    s._bfs = [-1] * tab.getNumCons()
+    return s
+
+
+# ---------------------------------------------------------------- fixtures
+
+def source_of(spec):
+    if "gen" in spec:
+        g = spec["gen"]
+        T = gen.tableau(g["kind"], g["m"], g["ns"], g["seed"])
+        return T, exact.from_array(T)
+    if "exact" in spec:
+        e = spec["exact"]
+        rows = exact.from_strings(e["z"], e["c"], e["b"], e["a"])
+        T = np.array([[float(x) for x in r] for r in rows])
+        return T, rows
+    T = np.asarray(spec["array"], dtype=np.float64)
+    return T, exact.from_array(T)
+
+
+def solve_fixture(name, spec, check_oracle=True):
+    T, rows = source_of(spec)
+    t = ref_tableau_from_rows(rows)
+    log = []
+    t0 = time.time()
+    s = LoggingSimplex(t, log)
+    init_pivots = len(log)
+    s.solve()
+    dt = time.time() - t0
+    seq = [[r, c] for r, c, _ in log]
+    nstd = sum(1 for _, _, k in log[init_pivots:] if k == "std")
+    fx = {
+        "name": name, "mode": "solve", **spec,
+        "m": int(T.shape[0] - 1), "n": int(T.shape[1] - 1),
+        "sha256": gen.digest(T),
+        "seq": seq, "nstd": nstd, "init_pivots": init_pivots,
+        "objective": fs(s.getObjValue()),
+        "objective_float": float(s.getObjValue()),
+        "bfs": list(s.getBasicSequence()),
+        "ref_seconds": round(dt, 4),
+    }
+    if T.size <= 400:
+        fx["final"] = [[fs(x) for x in row] for row in ref_rows(t)]
+    if check_oracle and init_pivots == 0:
+        orow = [list(r) for r in rows]
+        res = exact.solve(orow)
+        assert [list(p) for p in res["seq"]] == seq, f"{name}: oracle sequence differs"
+        assert res["nstd"] == nstd, f"{name}: oracle nstd differs"
+        assert fs(exact.objective(orow)) == fx["objective"], f"{name}: oracle objective"
+    print(f"{name}: {len(seq)} pivots ({nstd} std) in {dt:.3f}s obj={fx['objective_float']}",
+          flush=True)
+    return fx
+
+
+def standard_k_fixture(name, spec, k, check_oracle=True):
+    """k pivots of findPivotStandard(True) with no phase 1 / stall logic."""
+    T, rows = source_of(spec)
+    t = ref_tableau_from_rows(rows)
+    log = []
+    s = bare_simplex(t, log)
+    end = None
+    t0 = time.time()
+    for _ in range(k):
+        res = s.findPivotStandard(True)
+        if isinstance(res, str):
+            end = res
+            break
+    dt = time.time() - t0
+    seq = [[r, c] for r, c, _ in log]
+    fx = {
+        "name": name, "mode": "standard_k", "k": k, **spec,
+        "m": int(T.shape[0] - 1), "n": int(T.shape[1] - 1),
+        "sha256": gen.digest(T), "seq": seq, "end": end,
+        "objective": fs(t.getZ()), "objective_float": float(t.getZ()),
+        "ref_seconds": round(dt, 4),
+    }
+    if check_oracle:
+        orow = [list(r) for r in rows]
+        oseq = exact.run_standard(orow, k)
+        oend = oseq[-1] if oseq and isinstance(oseq[-1], str) else None
+        oseq = [list(p) for p in oseq if not isinstance(p, str)]
+        assert oseq == seq and oend == end, f"{name}: oracle sequence differs"
+        assert fs(exact.objective(orow)) == fx["objective"], f"{name}: oracle objective"
+    print(f"{name}: {len(seq)} std pivots end={end} in {dt:.3f}s", flush=True)
+    return fx
+
+
+def selection_fixture(name, spec, npiv):
+    """Reference findPivot* results (no pivot) at successive states of a
+    standard-rule walk: pins the selection rules, max-increase and find-all."""
+    T, rows = source_of(spec)
+    t = ref_tableau_from_rows(rows)
+    s = bare_simplex(t, [])
+    states = []
+    for _ in range(npiv):
+        st = {
+            "standard": s.findPivotStandard(False),
+            "min_index": s.findPivotMinIndex(False),
+            "max_increase": s.findPivotMaxIncrease(False),
+            "all": [list(p) for p in s.findPivotAll()],
+            "is_optimal": t.isOptimal(),
+            "is_unbounded": t.isUnbounded(),
+            "is_infeasible": t.isInfeasible(),
+            "is_degenerate": t.isDegenerate(),
+        }
+        bc = [0] * t.getNumCons()
+        st["is_canonical"] = t.isCanonical(bc)
+        st["bcols"] = bc
+        for k in ("standard", "min_index", "max_increase"):
+            if isinstance(st[k], tuple):
+                st[k] = list(st[k])
+        states.append(st)
+        res = s.findPivotStandard(True)
+        if isinstance(res, str):
+            break
+    print(f"{name}: {len(states)} selection states", flush=True)
+    return {"name": name, "mode": "selection", **spec,
+            "m": int(T.shape[0] - 1), "n": int(T.shape[1] - 1),
+            "sha256": gen.digest(T), "states": states}
+
+
+def kat_fixture():
+    """The reference's own known-answer pivot test (test_tableau.py:9-29,
+    :220-227) recorded as exact values."""
+    tab1a = exact.from_strings("0", ["-40", "-30", "0", "0"], ["12", "16"],
+                               [["1", "1", "1", "0"], ["2", "1", "0", "1"]])
+    t = ref_tableau_from_rows(tab1a)
+    t.pivot(1, 0)
+    after1 = ref_rows(t)
+    t.pivot(0, 1)
+    after2 = ref_rows(t)
+    return {"name": "kat_tab1", "mode": "kat",
+            "start": [[fs(x) for x in r] for r in tab1a],
+            "pivots": [[1, 0], [0, 1]],
+            "after": [[[fs(x) for x in r] for r in after1],
+                      [[fs(x) for x in r] for r in after2]]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true")
+    args = ap.parse_args()
+
+    small = {"kat": [kat_fixture()], "solve": [], "standard_k": [], "selection": []}
+    z, c, b, a = gen.beale_exact()
+    small["solve"].append(solve_fixture("beale", {"exact": {"z": z, "c": c, "b": b, "a": a}}))
+    for d in (3, 4, 5, 6, 8, 10):
+        small["solve"].append(solve_fixture(f"km_std_d{d}", {"array": gen.klee_minty(d).tolist()}))
+    for d in (4, 6, 8, 10):
+        small["solve"].append(solve_fixture(f"km_deg_d{d}",
+                                            {"array": gen.klee_minty(d, True).tolist()}))
+    for seed in range(1, 9):
+        small["solve"].append(solve_fixture(f"cfg1_mixed_s{seed}",
+                                            {"gen": {"kind": "mixed", "m": 8, "ns": 10, "seed": seed}}))
+    for seed in range(1, 5):
+        small["solve"].append(solve_fixture(f"cfg1_pos_s{seed}",
+                                            {"gen": {"kind": "pos", "m": 8, "ns": 10, "seed": seed}}))
+    for (m, ns) in ((16, 16), (24, 32), (32, 24), (40, 40)):
+        for seed in (11, 12, 13):
+            small["solve"].append(solve_fixture(f"mixed_{m}x{ns}_s{seed}",
+                                                {"gen": {"kind": "mixed", "m": m, "ns": ns, "seed": seed}}))
+    for (m, ns) in ((32, 32), (64, 64)):
+        for seed in (21, 22):
+            small["solve"].append(solve_fixture(f"pos_{m}x{ns}_s{seed}",
+                                                {"gen": {"kind": "pos", "m": m, "ns": ns, "seed": seed}}))
+    for seed in range(1, 7):
+        small["standard_k"].append(standard_k_fixture(
+            f"tall_64x16_s{seed}", {"gen": {"kind": "tall", "m": 64, "ns": 16, "seed": seed}}, 400))
+    small["standard_k"].append(standard_k_fixture(
+        "mixed_64x64_k120", {"gen": {"kind": "mixed", "m": 64, "ns": 64, "seed": 31}}, 120))
+    small["selection"].append(selection_fixture(
+        "sel_mixed_8x10", {"gen": {"kind": "mixed", "m": 8, "ns": 10, "seed": 3}}, 12))
+    small["selection"].append(selection_fixture(
+        "sel_tall_16x8", {"gen": {"kind": "tall", "m": 16, "ns": 8, "seed": 4}}, 12))
+    small["selection"].append(selection_fixture(
+        "sel_km_deg_d6", {"array": gen.klee_minty(6, True).tolist()}, 12))
+    small["selection"].append(selection_fixture(
+        "sel_beale", {"exact": {"z": z, "c": c, "b": b, "a": a}}, 12))
+    with open(os.path.join(OUT, "small.json"), "w") as f:
+        json.dump(small, f, separators=(",", ":"))
+
+    if args.big:
+        big = {"solve": [], "standard_k": []}
+        big["solve"].append(solve_fixture(
+            "cfg2_pos_512x512_s7", {"gen": {"kind": "pos", "m": 512, "ns": 512, "seed": 7}},
+            check_oracle=False))
+        big["standard_k"].append(standard_k_fixture(
+            "cfg2_mixed_512x512_s7_k64", {"gen": {"kind": "mixed", "m": 512, "ns": 512, "seed": 7}},
+            64, check_oracle=False))
+        with open(os.path.join(OUT, "big.json"), "w") as f:
+            json.dump(big, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+    main()

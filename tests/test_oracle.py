@@ -1,0 +1,139 @@
+"""Pin the oracles to the reference (CPU only).
+
+Golden vectors were captured by running the reference itself in the build
+container (tests/golden/make_golden.py).  Both oracles must reproduce them:
+  * oracle/exact.py  (Fraction restatement): identical pivot sequences,
+    identical exact objectives, identical final tableaux;
+  * oracle/lp_f64.c  (float64 restatement with the engine's semantics):
+    identical pivot sequences, objective within 1e-9 relative.
+"""
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from conftest import fixture_exact, fixture_input, load_golden
+
+from lpsol_amd import generators as gen
+from oracle import exact
+from oracle.f64 import F64Tableau
+
+SMALL = load_golden("small.json")
+BIG = load_golden("big.json")
+REL = 1e-9   # north star: objective within 1e-9 relative of the rational answer
+
+
+def _ids(fxs):
+    return [fx["name"] for fx in fxs]
+
+
+def test_kat_reference_pivot_pair():
+    """tableau.py test_pivot (test_tableau.py:220-227) on the exact oracle."""
+    kat = SMALL["kat"][0]
+    T = [[Fraction(x) for x in r] for r in kat["start"]]
+    for (r, c), after in zip(kat["pivots"], kat["after"]):
+        exact.pivot(T, r, c)
+        assert T == [[Fraction(x) for x in row] for row in after]
+
+
+@pytest.mark.parametrize("fx", SMALL["solve"] + BIG["solve"] + SMALL["standard_k"] + BIG["standard_k"],
+                         ids=_ids(SMALL["solve"] + BIG["solve"] + SMALL["standard_k"] + BIG["standard_k"]))
+def test_fixture_input_pinned(fx):
+    """the generator / hand-built inputs are byte-identical to the captured ones"""
+    assert gen.digest(fixture_input(fx)) == fx["sha256"]
+
+
+@pytest.mark.parametrize("fx", SMALL["solve"], ids=_ids(SMALL["solve"]))
+def test_exact_solve_matches_reference(fx):
+    T = fixture_exact(fx)
+    res = exact.solve(T)
+    assert [list(p) for p in res["seq"]] == fx["seq"]
+    assert res["nstd"] == fx["nstd"]
+    assert exact.frac_str(exact.objective(T)) == fx["objective"]
+    if "final" in fx:
+        assert T == [[Fraction(x) for x in row] for row in fx["final"]]
+    bfs = [-1] * (len(T) - 1)
+    ok, bcols = exact.is_canonical(fixture_exact(fx))
+    assert ok
+    bfs = list(bcols)
+    for r, c in res["seq"]:
+        bfs[r] = c
+    assert bfs == fx["bfs"]
+
+
+@pytest.mark.parametrize("fx", SMALL["standard_k"], ids=_ids(SMALL["standard_k"]))
+def test_exact_standard_k_matches_reference(fx):
+    T = fixture_exact(fx)
+    seq = exact.run_standard(T, fx["k"])
+    end = seq[-1] if seq and isinstance(seq[-1], str) else None
+    assert [list(p) for p in seq if not isinstance(p, str)] == fx["seq"]
+    assert end == fx["end"]
+    assert exact.frac_str(exact.objective(T)) == fx["objective"]
+
+
+@pytest.mark.parametrize("fx", SMALL["selection"], ids=_ids(SMALL["selection"]))
+def test_exact_selection_rules_match_reference(fx):
+    """findPivotStandard/MinIndex/MaxIncrease/All and the form checks at every
+    state of a standard-rule walk."""
+    T = fixture_exact(fx)
+    for st in fx["states"]:
+        def norm(x):
+            return list(x) if isinstance(x, tuple) else x
+        assert norm(exact.find_standard(T)) == st["standard"]
+        assert norm(exact.find_min_index(T)) == st["min_index"]
+        assert norm(exact.find_max_increase(T)) == st["max_increase"]
+        assert [list(p) for p in exact.find_all(T)] == st["all"]
+        assert exact.is_optimal(T) == st["is_optimal"]
+        assert exact.is_unbounded(T) == st["is_unbounded"]
+        assert exact.is_infeasible(T) == st["is_infeasible"]
+        assert exact.is_degenerate(T) == st["is_degenerate"]
+        ok, bcols = exact.is_canonical(T)
+        assert ok == st["is_canonical"]
+        if ok or any(b != 0 for b in st["bcols"]):
+            assert bcols == st["bcols"]
+        res = exact.find_standard(T)
+        if isinstance(res, str):
+            break
+        exact.pivot(T, *res)
+
+
+@pytest.mark.parametrize("fx", SMALL["solve"] + BIG["solve"], ids=_ids(SMALL["solve"] + BIG["solve"]))
+def test_f64_oracle_solve_matches_reference(fx):
+    t = F64Tableau(fixture_input(fx))
+    st, log, nstd = t.solve()
+    assert st == 1
+    assert log.tolist() == fx["seq"]
+    assert nstd == fx["nstd"]
+    obj = float(Fraction(fx["objective"]))
+    assert abs(t.objective() - obj) <= REL * max(1.0, abs(obj))
+
+
+@pytest.mark.parametrize("fx", SMALL["standard_k"] + BIG["standard_k"],
+                         ids=_ids(SMALL["standard_k"] + BIG["standard_k"]))
+def test_f64_oracle_standard_k_matches_reference(fx):
+    t = F64Tableau(fixture_input(fx))
+    st, log = t.run(0, fx["k"])
+    assert log.tolist() == fx["seq"]
+    assert (fx["end"] == "optimal") == (st == 1)
+    obj = float(Fraction(fx["objective"]))
+    assert abs(t.objective() - obj) <= REL * max(1.0, abs(obj))
+
+
+def test_f64_oracle_cycling_without_switch():
+    """Beale's LP cycles under the pure standard rule: the stall switch of
+    solve() is what ends it."""
+    t = F64Tableau(gen.beale())
+    st, log = t.run(0, 40)
+    assert st == 0 and len(log) == 40          # still pivoting: a cycle
+    assert [tuple(p) for p in log[:6]] == [tuple(p) for p in log[6:12]]
+
+
+def test_generator_is_counter_based():
+    """any row block can be generated independently (sharded ranks)"""
+    full = gen.tableau("tall", 40, 24, 5)
+    parts = [gen.rows("tall", 40, 24, 5, a, b) for a, b in ((0, 7), (7, 20), (20, 41))]
+    assert np.array_equal(full, np.vstack(parts))
+    T = gen.tableau("mixed", 16, 16, 3)
+    assert np.all(T[1:, 0] > 0) and np.all(T[0, 1:17] < 0)
+    assert np.array_equal(T[1:, 17:], np.eye(16))
+    assert np.all(np.abs(T * 64 - np.round(T * 64)) == 0)      # dyadic k/64
