@@ -133,10 +133,18 @@ int lp_pivot_log(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count);
 /* Objective value getZ() = -T[0][0] (tableau.py:82-84, simplex.py:175-179). */
 int lp_objective(lp_handle *h, double *z);
 
-/* Device-time accounting of the rank-1 update kernel (for the roofline):
- * when enabled, each update launch is bracketed by HIP events on the stream
- * it runs on.  lp_update_time returns the summed milliseconds and launches
- * since the last reset. */
+/* Pivots deferred into one sweep of the tableau (1..32, default 8).  Each
+ * pivot's selection and pivot row use current values computed on the fly; the
+ * rank-1 eliminations of `pivots_per_sweep` pivots are applied to the stored
+ * tableau in one pass (the same float64 operations in the same order, so the
+ * results are identical for every setting).  1 = immediate elimination. */
+int lp_set_block(lp_handle *h, int pivots_per_sweep);
+int lp_get_block(const lp_handle *h, int *pivots_per_sweep);
+
+/* Device-time accounting of the elimination sweep kernel (for the roofline):
+ * when enabled, each sweep launch is bracketed by HIP events on the stream it
+ * runs on.  lp_update_time returns the summed milliseconds and launches since
+ * the last reset. */
 int lp_profile(lp_handle *h, int enable);
 int lp_update_time(lp_handle *h, double *ms, int64_t *launches);
 

@@ -13,39 +13,47 @@ constexpr int MODE_RUN = 0;    // fixed rule, no stall logic (findPivot*, lp_run
 constexpr int MODE_SOLVE = 1;  // Simplex.solve semantics (simplex.py:110-148)
 
 // k_ratio modes
-constexpr int RATIO_FULL = 0;   // single device: pick the leaving row directly
-constexpr int RATIO_LOCAL = 1;  // sharded: publish this rank's minimum ratio only
-constexpr int RATIO_CHECK = 2;  // single device: validate a given row (Simplex.pivot)
+constexpr int RATIO_FULL = 0;   // single device: publish per-block candidates
+constexpr int RATIO_LOCAL = 1;  // sharded: also reduce this rank's minimum ratio
+constexpr int RATIO_CHECK = 2;  // validate a given row (Simplex.pivot)
+
+// where k_prow finds the leaving row
+constexpr int RSRC_RECORDS = 0;  // combine k_ratio's per-block records
+constexpr int RSRC_GIVEN = 1;    // dR[t] set by the caller (Tableau.pivot / Simplex.pivot)
+constexpr int RSRC_SLOTS = 2;    // sharded: the gathered rank slots
 
 // k_pick modes (sharded)
 constexpr int PICK_RATIO = 0;     // first local row within the tie band of the global min
 constexpr int PICK_CHECK = 1;     // owner validates the requested row (Simplex.pivot)
 constexpr int PICK_EXPLICIT = 2;  // owner contributes the requested row (Tableau.pivot)
 
+constexpr int BMAX = 32;           // most pivots deferred into one sweep
 constexpr int RATIO_THREADS = 256;
 constexpr int RATIO_CHUNK = 256;   // rows per ratio block (one per thread)
-constexpr int UPD_ROWS = 64;       // rows per update block
-constexpr int UPD_UNROLL = 4;      // rows in flight per wave
+constexpr int PROW_THREADS = 256;  // columns per pivot-row block (one per thread)
+constexpr int SWEEP_ROWS = 64;     // rows per sweep block
+constexpr int SWEEP_UNROLL = 4;    // rows in flight per wave
 constexpr int ENTER_THREADS = 1024;
 constexpr int SLOT_HDR = 8;        // doubles of header in front of an exchanged row
 
 constexpr long long NONE = 0x7fffffffffffffffLL;
 
 // Device-resident control block: the pivot loop's whole state lives here so
-// a batch of pivots is enqueued without host round trips.
+// batches of pivots are enqueued without host round trips.
 struct Ctl {
     int status;          // lp_status of the current step; LP_PIVOTED = keep going
     int mode;            // MODE_RUN / MODE_SOLVE
     int rule;            // lp_rule for the next selection
-    int pad0;
+    int chain;           // 1: pivots follow each other in one call
     long long r, c;      // current pivot (global constraint index, variable index)
     long long npiv;      // pivots performed since the last reset
     long long nstd;      // of which with the standard rule (solve mode)
     long long stuck;     // steps_stuck (simplex.py:119)
     long long cap;       // pivot cap (< 0: none)
+    long long ndef[2];   // pivots of the current group (by group parity) not yet swept
     double z0;           // obj_val at the start of solve (simplex.py:118)
-    unsigned ticket;     // last-block ticket of k_ratio
-    unsigned pad1;
+    unsigned ticket;     // last-block ticket of k_ratio (LOCAL / CHECK modes)
+    unsigned pad;
 };
 
 // Per-block ratio-test summary.
@@ -56,22 +64,37 @@ struct Rec {
     double pad;
 };
 
-// Row-exchange slot: header + one raw tableau row (ld doubles).
-//   hdr[0] = candidate global constraint index (NONE if none), as int64 bits
-//   hdr[1] = code (0, LP_BAD_PIVOT or LP_ZERO_PIVOT), as int64 bits
+// Per-block entering-column summary over a slice of row 0.
+struct ERec {
+    double l;            // slice minimum of c_j
+    long long i;         // first column within the tie band of l
+    double q;            // its value
+    long long fneg;      // first column with c_j < -tol.cost
+};
+
+// Deferred pivots: pivot s (0 <= s < ndef) of the current group is
+//   (dR[s] local row or -1, dC[s] tableau column), multipliers M[i*BMAX + s]
+//   = value of (i, dC[s]) just before pivot s, normalised row P[s*ld + j].
+// The current value of any element is its stored value with pivots 0..t-1
+// applied in order by upd() (kernels.hip) -- the sweep writes exactly that.
 struct Args {
     double *T;           // local tableau: row 0 + local constraint rows
-    double *P;           // normalised pivot row (ld doubles)
-    double *mult;        // column snapshot, one per local row
+    double *row0;        // current row 0 (ld doubles)
+    double *col0;        // current column 0 of the local rows (rows doubles)
+    double *M;           // rows x BMAX multipliers (row-major: a row's are contiguous)
+    double *P;           // BMAX x ld normalised pivot rows
+    long long *dR;       // BMAX local pivot rows (-1: another rank's row)
+    long long *dC;       // BMAX pivot columns (tableau index)
     Ctl *ctl;
     long long *log;      // (r, c) per pivot
     Rec *rec;
+    ERec *erec;
     double *xg;          // sharded: this rank's / the global minimum ratio (1 double)
     double *xs;          // sharded: send slot (SLOT_HDR + ld)
     double *xr;          // sharded: gathered slots (nranks x (SLOT_HDR + ld))
     long long logcap;
     long long m, n;      // GLOBAL problem size
-    long long ld;        // leading dimension (doubles)
+    long long ld;        // leading dimension of T, P, row0 (doubles)
     long long rows;      // local rows incl. row 0
     long long rb;        // first global constraint row of this rank
     long long rc;        // local constraint rows
@@ -80,17 +103,26 @@ struct Args {
     lp_tol tol;
 };
 
-// launch wrappers (kernels.hip)
-hipError_t launch_reset(hipStream_t s, Ctl *ctl, int mode, int rule, long long cap, long long r,
-                        long long c, const double *T);
+// launch wrappers (kernels.hip).  t = index of the pivot within its group
+// (known to the host, which enqueues the groups); grp = group parity.
+hipError_t launch_reset(hipStream_t s, const Args &A, int mode, int rule, int chain, long long cap,
+                        long long r, long long c);
+hipError_t launch_load_eager(hipStream_t s, const Args &A);
 hipError_t launch_enter(hipStream_t s, const Args &A);
-hipError_t launch_ratio(hipStream_t s, const Args &A, int mode, long long check_local_row);
-hipError_t launch_pick(hipStream_t s, const Args &A, int mode);
-hipError_t launch_gather(hipStream_t s, const Args &A);
-hipError_t launch_prow(hipStream_t s, const Args &A);
-hipError_t launch_prow_sharded(hipStream_t s, const Args &A);
-hipError_t launch_update(hipStream_t s, const Args &A);
+hipError_t launch_ratio(hipStream_t s, const Args &A, int t, int grp, int mode, int from_erec,
+                        long long check_local_row);
+hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
+hipError_t launch_gather(hipStream_t s, const Args &A, int t);
+hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max);  // nd_max >= ndef
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
-int ratio_blocks(long long rows);
+__host__ __device__ inline int ratio_blocks(long long rows)
+{
+    return (int)((rows - 1 + RATIO_CHUNK - 1) / RATIO_CHUNK);
+}
+__host__ __device__ inline int prow_blocks(long long ld)
+{
+    return (int)((ld + PROW_THREADS - 1) / PROW_THREADS);
+}
 
 }  // namespace lpk

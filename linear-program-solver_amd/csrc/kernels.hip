@@ -1,23 +1,43 @@
 // Device kernels of the dense simplex pivot engine (gfx950 / CDNA4).
 //
-// One pivot, single device = four launches, all decisions on device:
-//   k_enter   entering-column scan of row 0          simplex.py:228-232 / :262-267
-//   k_ratio   min-ratio test + multiplier snapshot    simplex.py:235-246 / :270-281
-//   k_prow    normalised pivot row P                  tableau.py:302 (rowDiv)
-//   k_update  rank-1 elimination of every other row  tableau.py:303-308 -> :269-289
-// Row-sharded (one rank per GPU) inserts the exchange:
-//   k_enter, k_ratio(LOCAL) -> allreduce-min(g) -> k_pick -> allgather(slots)
-//   -> k_prow_sharded -> k_update
-// Float semantics are fixed in oracle/lp_f64.c's header and must stay
-// bit-identical to it (tests/test_gpu_parity.py compares whole tableaux).
+// Deferred ("blocked") pivots.  A pivot is selected and its normalised row
+// computed from CURRENT values, but the rank-1 elimination of the whole
+// tableau is postponed: up to BMAX pivots (a "group") are later applied in
+// one sweep that reads and writes the tableau once (a rank-B update: B FMAs
+// per 16 bytes of HBM traffic instead of 1).  Every element goes through
+// exactly the same float64 operations, in the same order, as with an
+// immediate update (oracle/lp_f64.c) -- upd() below is that operation -- so
+// results are bit-identical for any group size B (B = 1 is the plain pivot).
+//
+// Per pivot t of a group (single device), two launches:
+//   k_ratio   combines k_prow's row-0 summaries into the entering column
+//             (every block redundantly: the summaries are tiny), then the
+//             current column C (stored value + deferred pivots 0..t-1) ->
+//             multipliers M[t] and per-block min-ratio summaries
+//                                  simplex.py:228-232 / :262-267, :235-246 / :270-281
+//   k_prow    combines the ratio summaries into the leaving row (again in
+//             every block), current pivot row / a -> P[t]; pivot t applied to
+//             row 0 and column 0 (kept current eagerly); per-block row-0
+//             summaries for the next entering column
+//                                  tableau.py:300-303
+// Every B pivots (and at the end of every call):
+//   k_sweep   T <- T with pivots 0..ndef-1 applied  tableau.py:305-308 -> :269-289
+// No atomics or grid-wide hand-offs on this path: each kernel consumes the
+// previous kernel's records after the kernel boundary.
+// Row-sharded (one rank per GPU) replaces the leaving-row choice with
+//   k_ratio(LOCAL) -> allreduce-min(g) -> k_pick -> allgather(slots) -> k_prow
 //
 // Local storage: row 0 (objective, replicated on every rank) + this rank's
 // constraint rows, row-major, leading dimension ld (a multiple of 64 doubles
-// = 512 B, so every row starts on a cache-line boundary and 16-byte vector
-// accesses are aligned).
+// = 512 B: every row starts on a cache-line boundary, 16-byte accesses are
+// aligned).
 #include "engine.h"
 
 namespace lpk {
+
+// ---------------------------------------------------------------------------
+// reductions
+// ---------------------------------------------------------------------------
 
 __device__ __forceinline__ double wave_min(double v)
 {
@@ -63,9 +83,48 @@ __device__ long long block_min_ll(long long v, long long *scratch)
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// cross-block hand-off (only k_ratio's LOCAL / CHECK modes): payload stored
+// write-through (sc1), every storing wave drains, one lane per block takes an
+// agent-scope ticket; the last arriver reads with sc1 loads
+// (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH "Valid forms" row 1).
+// ---------------------------------------------------------------------------
+
+template <typename T>
+__device__ __forceinline__ void st_sc1(T *p, T v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T *p)
+{
+    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// every thread calls; returns true in the last block to arrive
+__device__ bool arrive_last(unsigned *ticket, int *s_flag)
+{
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (t == gridDim.x - 1);
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+// ---------------------------------------------------------------------------
+// numerics shared by every kernel
+// ---------------------------------------------------------------------------
+
 __device__ __forceinline__ double tie_band(double g, double tie) { return g + tie * fabs(g); }
 
-// ratio of one constraint row for the entering column; ok=false if a <= tol.pivot
+// ratio of one constraint row; ok=false if a <= tol.pivot   (simplex.py:273-276)
 __device__ __forceinline__ double row_ratio(double a, double b, const lp_tol &tol, bool &ok)
 {
     ok = a > tol.pivot;
@@ -73,7 +132,60 @@ __device__ __forceinline__ double row_ratio(double a, double b, const lp_tol &to
     return ok ? num / a : 0.0;
 }
 
-// local row of global constraint r, or -1 if another rank holds it
+// one pivot applied to one element (row li, value x before the pivot):
+// the pivot row becomes P, every other row gets fma(-f, P[j], x).  In the
+// pivot column x == f and P == 1, so the result is exactly +0 (the unit
+// column).  A zero multiplier leaves x unchanged (tableau.py:272 skips such
+// rows; in float64 only the sign of a zero x could differ, which nothing
+// downstream can observe), so no branch is needed.
+__device__ __forceinline__ double upd(long long li, long long R, double f, double p, double x)
+{
+    return li == R ? p : fma(-f, p, x);
+}
+
+// current value of (li, j): stored value x with deferred pivots 0..t-1
+// (generic form, used on rare paths)
+__device__ double current(const Args &A, int t, long long li, long long j, double x)
+{
+    for (int s = 0; s < t; ++s)
+        x = upd(li, A.dR[s], A.M[li * BMAX + s], A.P[s * A.ld + j], x);
+    return x;
+}
+
+// current value of (li, C) for the thread's own row: the multipliers of the
+// row are loaded as one contiguous run; dR[s] and P[s][C] come staged in LDS
+template <int TP>
+__device__ __forceinline__ double current_col(const Args &A, int t, long long li, double x,
+                                              const long long *sR, const double *sPc)
+{
+    if constexpr (TP > 0) {
+        double mv[TP];
+#pragma unroll
+        for (int s = 0; s < TP; ++s) mv[s] = A.M[li * BMAX + s];
+#pragma unroll
+        for (int s = 0; s < TP; ++s)
+            if (s < t) x = upd(li, sR[s], mv[s], sPc[s], x);
+    }
+    return x;
+}
+
+// current value of (R, j) for the thread's own column of one row R: the TP
+// pivot-row values are independent coalesced loads issued together
+template <int TP>
+__device__ __forceinline__ double current_row(const Args &A, int t, long long R, long long j,
+                                              double x)
+{
+    if constexpr (TP > 0) {
+        double pv[TP];
+#pragma unroll
+        for (int s = 0; s < TP; ++s) pv[s] = A.P[s * A.ld + j];
+#pragma unroll
+        for (int s = 0; s < TP; ++s)
+            if (s < t) x = upd(R, A.dR[s], A.M[R * BMAX + s], pv[s], x);
+    }
+    return x;
+}
+
 __device__ __forceinline__ long long local_of(const Args &A, long long r)
 {
     return (r >= A.rb && r < A.rb + A.rc) ? r - A.rb + 1 : -1;
@@ -86,62 +198,58 @@ __device__ __forceinline__ double as_d(long long v) { return __longlong_as_doubl
 // control
 // ---------------------------------------------------------------------------
 
-__global__ void k_reset(Ctl *ctl, int mode, int rule, long long cap, long long r, long long c,
-                        const double *T)
+__global__ void k_reset(Args A, int mode, int rule, int chain, long long cap, long long r,
+                        long long c)
 {
+    Ctl *ctl = A.ctl;
     ctl->status = LP_PIVOTED;
     ctl->mode = mode;
     ctl->rule = rule;
+    ctl->chain = chain;
     ctl->cap = cap;
     ctl->r = r;
     ctl->c = c;
     ctl->npiv = 0;
     ctl->nstd = 0;
     ctl->stuck = 0;
-    ctl->z0 = -T[0];
+    ctl->ndef[0] = 0;
+    ctl->ndef[1] = 0;
+    ctl->z0 = -A.row0[0];
     ctl->ticket = 0;
+    A.dR[0] = r >= 0 ? local_of(A, r) : -1;
 }
 
-// ---------------------------------------------------------------------------
-// K1: entering column (one workgroup of 1024 threads over row 0)
-// ---------------------------------------------------------------------------
+// row0 / col0 <- the stored tableau (after an upload)
+__global__ void k_load_eager(Args A)
+{
+    const long long g = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long j = g; j < A.ld; j += stride) A.row0[j] = A.T[j];
+    for (long long i = g; i < A.rows; i += stride) A.col0[i] = A.T[i * A.ld];
+}
 
+// entering column from the current row 0 (one workgroup): first pivot of a call
 __global__ void __launch_bounds__(ENTER_THREADS) k_enter(Args A)
 {
     __shared__ double sd[16];
     __shared__ long long sl[16];
-    __shared__ int s_rule, s_go;
+    __shared__ int s_go;
     Ctl *ctl = A.ctl;
     if (threadIdx.x == 0) {
         int go = ctl->status == LP_PIVOTED;
-        int rule = ctl->rule;
-        if (go && ctl->mode == MODE_SOLVE) {
-            // stall bookkeeping for the pivot just done (simplex.py:132-137)
-            if (ctl->npiv > 0 && rule == LP_RULE_STANDARD) {
-                const double z = -A.T[0];
-                const double z0 = ctl->z0;
-                if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) ctl->stuck += 1;
-                else ctl->stuck = 0;
-            }
-            // switch to the min-index rule once stuck (simplex.py:123,138)
-            if (rule == LP_RULE_STANDARD && ctl->stuck >= A.m + A.n) {
-                rule = LP_RULE_MIN_INDEX;
-                ctl->rule = rule;
-            }
-        }
         if (go && ctl->cap >= 0 && ctl->npiv >= ctl->cap) {
             ctl->status = LP_CAP_REACHED;
             go = 0;
         }
-        s_rule = rule;
         s_go = go;
     }
     __syncthreads();
     if (!s_go) return;
-    const double *c0 = A.T;
+    const int rule = ctl->rule;
+    const double *c0 = A.row0;
     const long long n = A.n;
     long long j = NONE;
-    if (s_rule == LP_RULE_MIN_INDEX) {
+    if (rule == LP_RULE_MIN_INDEX) {
         for (long long k = 1 + threadIdx.x; k <= n; k += blockDim.x)
             if (c0[k] < -A.tol.cost) { j = k; break; }
         j = block_min_ll(j, sl);
@@ -162,75 +270,137 @@ __global__ void __launch_bounds__(ENTER_THREADS) k_enter(Args A)
     }
 }
 
+// entering column from k_prow's per-block row-0 summaries (block-wide, every
+// block gets the same answer): two-pass semantics of oracle/lp_f64.c's
+// entering().  The first summary block inside the global band holds the
+// answer -- its own candidate, or a rescan of its slice of row 0.
+__device__ long long combine_entering(const Args &A, int rule, double *sd, long long *sl)
+{
+    const unsigned nb = (unsigned)prow_blocks(A.ld);
+    if (rule == LP_RULE_MIN_INDEX) {
+        long long j = NONE;
+        for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) {
+            const long long f = A.erec[b].fneg;
+            j = f < j ? f : j;
+        }
+        return block_min_ll(j, sl);
+    }
+    double g = INFINITY;
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) g = fmin(g, A.erec[b].l);
+    g = block_min(g, sd);
+    if (!(g < -A.tol.cost)) return NONE;
+    const double thr = tie_band(g, A.tol.cost_tie);
+    long long bsel = NONE;
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x)
+        if (A.erec[b].l <= thr) { bsel = b; break; }
+    bsel = block_min_ll(bsel, sl);
+    if (A.erec[bsel].q <= thr) return A.erec[bsel].i;
+    long long best = NONE;
+    const long long k0 = bsel * (long long)PROW_THREADS;
+    for (long long k = k0 + threadIdx.x; k < k0 + PROW_THREADS; k += blockDim.x)
+        if (k >= 1 && k <= A.n && A.row0[k] <= thr) { best = k; break; }
+    return block_min_ll(best, sl);
+}
+
 // ---------------------------------------------------------------------------
-// K2: ratio test over this rank's constraint rows + multiplier snapshot.
-//   Each block owns RATIO_CHUNK consecutive rows and publishes
-//   (local min l_b, first row within the tie band of l_b, its ratio).  The
-//   last block to arrive combines them in row order.  Because every earlier
-//   row of a block has a ratio above tie_band(l_b) >= tie_band(g), the first
-//   block with l_b <= tie_band(g) holds the answer: its own candidate if that
-//   is inside the global band, otherwise a rescan of that block alone.  The
-//   result equals the two-pass scan of oracle/lp_f64.c for any scheduling.
+// K1: entering column (chained pivots), ratio test over this rank's
+// constraint rows, multiplier snapshot M[t], per-block summaries
+//   (local min l_b, first row within the tie band of l_b, its ratio).
+// Every earlier row of a block has a ratio above tie_band(l_b) >=
+// tie_band(g), so the first block with l_b <= tie_band(g) holds the leaving
+// row: its own candidate if inside the global band, else a rescan of that
+// block alone -- equal to the two-pass scan of oracle/lp_f64.c.
 // ---------------------------------------------------------------------------
 
 // first local row in [li0, li1) with ratio <= thr (block-wide), NONE if none
-__device__ long long rescan_rows(const Args &A, long long C, long long li0, long long li1,
+__device__ long long rescan_rows(const Args &A, int t, long long C, long long li0, long long li1,
                                  double thr, long long *scratch)
 {
     long long best = NONE;
     for (long long li = li0 + threadIdx.x; li < li1; li += blockDim.x) {
         bool ok;
-        const double *t = A.T + li * A.ld;
-        const double q = row_ratio(t[C], t[0], A.tol, ok);
+        const double a = current(A, t, li, C, A.T[li * A.ld + C]);
+        const double q = row_ratio(a, A.col0[li], A.tol, ok);
         if (ok && q <= thr) { best = li; break; }
     }
     return block_min_ll(best, scratch);
 }
 
-// first local row within tie_band(g) using the block records (block-wide)
-__device__ long long pick_from_records(const Args &A, long long C, double g, long long *scratch)
+// first local row within tie_band(g), from the ratio summaries (block-wide)
+__device__ long long pick_from_records(const Args &A, int t, long long C, double g,
+                                       long long *scratch)
 {
     const double thr = tie_band(g, A.tol.ratio_tie);
-    const unsigned nb = (unsigned)((A.rc + RATIO_CHUNK - 1) / RATIO_CHUNK);
+    const unsigned nb = (unsigned)ratio_blocks(A.rows);
     long long bsel = NONE;
-    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) {
-        const double l = __hip_atomic_load(&A.rec[b].l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (l <= thr) { bsel = b; break; }
-    }
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x)
+        if (A.rec[b].l <= thr) { bsel = b; break; }
     bsel = block_min_ll(bsel, scratch);
     if (bsel == NONE) return NONE;
-    const double qb = __hip_atomic_load(&A.rec[bsel].q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const long long ib = __hip_atomic_load(&A.rec[bsel].i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (qb <= thr) return ib;
+    if (A.rec[bsel].q <= thr) return A.rec[bsel].i;
     const long long b0 = 1 + bsel * RATIO_CHUNK;
-    return rescan_rows(A, C, b0, min(b0 + RATIO_CHUNK, A.rows), thr, scratch);
+    return rescan_rows(A, t, C, b0, min(b0 + RATIO_CHUNK, A.rows), thr, scratch);
 }
 
-__global__ void __launch_bounds__(RATIO_THREADS) k_ratio(Args A, int mode, long long check_row)
+// minimum over the ratio summaries (block-wide)
+__device__ double records_min(const Args &A, double *sd)
+{
+    const unsigned nb = (unsigned)ratio_blocks(A.rows);
+    double g = INFINITY;
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) g = fmin(g, A.rec[b].l);
+    return block_min(g, sd);
+}
+
+template <int TP>
+__global__ void __launch_bounds__(RATIO_THREADS)
+k_ratio(Args A, int t, int grp, int mode, int from_erec, long long check_row)
 {
     __shared__ double sd[16];
     __shared__ long long sl[16];
+    __shared__ long long sR[TP > 0 ? TP : 1];
+    __shared__ double sPc[TP > 0 ? TP : 1];
     __shared__ double s_q;
     __shared__ int s_last;
     Ctl *ctl = A.ctl;
+    // the previous group's sweep is complete (stream order): recycle its counter
+    if (t == 0 && blockIdx.x == 0 && threadIdx.x == 0) ctl->ndef[grp ^ 1] = 0;
     if (ctl->status != LP_PIVOTED) {
         if (mode == RATIO_LOCAL && blockIdx.x == 0 && threadIdx.x == 0) *A.xg = INFINITY;
         return;
     }
-    const long long C = ctl->c + 1;
+    long long C;
+    if (from_erec) {
+        if (ctl->cap >= 0 && ctl->npiv >= ctl->cap) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_CAP_REACHED;
+            if (mode == RATIO_LOCAL && blockIdx.x == 0 && threadIdx.x == 0) *A.xg = INFINITY;
+            return;
+        }
+        C = combine_entering(A, ctl->rule, sd, sl);
+        if (C == NONE) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_OPTIMAL;
+            if (mode == RATIO_LOCAL && blockIdx.x == 0 && threadIdx.x == 0) *A.xg = INFINITY;
+            return;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctl->c = C - 1;
+    } else {
+        C = ctl->c + 1;
+    }
+    if (threadIdx.x < TP && threadIdx.x < t) {
+        sR[threadIdx.x] = A.dR[threadIdx.x];
+        sPc[threadIdx.x] = A.P[threadIdx.x * A.ld + C];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.M[t] = A.row0[C];   // row 0's multiplier
+    __syncthreads();
+
     const long long li0 = 1 + (long long)blockIdx.x * RATIO_CHUNK;
     const long long li1 = min(li0 + RATIO_CHUNK, A.rows);
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.mult[0] = A.T[C];
-
-    // one row per thread (RATIO_CHUNK == blockDim.x)
-    const long long li = li0 + threadIdx.x;
+    const long long li = li0 + threadIdx.x;      // one row per thread
     bool ok = false;
     double q = 0.0;
     if (li < li1) {
-        const double *t = A.T + li * A.ld;
-        const double a = t[C];
-        A.mult[li] = a;
-        q = row_ratio(a, t[0], A.tol, ok);
+        const double a = current_col<TP>(A, t, li, A.T[li * A.ld + C], sR, sPc);
+        A.M[li * BMAX + t] = a;
+        q = row_ratio(a, A.col0[li], A.tol, ok);
     }
     const double lb = block_min(ok ? q : INFINITY, sd);
     long long ib = NONE;
@@ -239,60 +409,49 @@ __global__ void __launch_bounds__(RATIO_THREADS) k_ratio(Args A, int mode, long 
     __syncthreads();
     if (ib != NONE && li == ib) s_q = q;
     __syncthreads();
-    // publish: one lane stores the record, releases it, then takes a ticket
-    // (agent-scope release/acquire, cdna_hip_programming.md Guideline 16)
-    if (threadIdx.x == 0) {
-        A.rec[blockIdx.x].l = lb;
-        A.rec[blockIdx.x].i = ib;
-        A.rec[blockIdx.x].q = s_q;
-        __threadfence();
-        const unsigned t = atomicAdd(&ctl->ticket, 1u);
-        s_last = (t == gridDim.x - 1);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();  // acquire the other blocks' records
-
-    double g = INFINITY;
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
-        g = fmin(g, __hip_atomic_load(&A.rec[b].l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    g = block_min(g, sd);
-
-    if (mode == RATIO_LOCAL) {
-        if (threadIdx.x == 0) { *A.xg = g; ctl->ticket = 0; }
-        return;
-    }
-    if (mode == RATIO_CHECK) {
-        // Simplex.pivot(r, c): row r must attain the minimum ratio (simplex.py:204-215)
+    if (mode == RATIO_FULL) {
         if (threadIdx.x == 0) {
-            const double *t = A.T + check_row * A.ld;
-            bool okr;
-            const double qr = row_ratio(t[C], t[0], A.tol, okr);
-            if (t[C] == 0.0) ctl->status = LP_ZERO_PIVOT;
-            else if (!(g < INFINITY) || !okr || !(qr <= tie_band(g, A.tol.ratio_tie)))
-                ctl->status = LP_BAD_PIVOT;
-            ctl->ticket = 0;
+            A.rec[blockIdx.x].l = lb;
+            A.rec[blockIdx.x].i = ib;
+            A.rec[blockIdx.x].q = s_q;
         }
         return;
     }
-    if (!(g < INFINITY)) {
-        if (threadIdx.x == 0) { ctl->status = LP_UNBOUNDED; ctl->ticket = 0; }
-        return;
-    }
-    const long long win = pick_from_records(A, C, g, sl);
+    // LOCAL / CHECK: the last block needs every summary within this launch
     if (threadIdx.x == 0) {
-        ctl->r = win - 1 + A.rb;
-        ctl->ticket = 0;
+        st_sc1(&A.rec[blockIdx.x].l, lb);
+        st_sc1(&A.rec[blockIdx.x].i, ib);
+        st_sc1(&A.rec[blockIdx.x].q, (double)s_q);
+    }
+    if (!arrive_last(&ctl->ticket, &s_last)) return;
+    double g = INFINITY;
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) g = fmin(g, ld_sc1(&A.rec[b].l));
+    g = block_min(g, sd);
+    if (threadIdx.x == 0) {
+        if (mode == RATIO_LOCAL) {
+            *A.xg = g;
+        } else {
+            // Simplex.pivot(r, c): row r must attain the minimum ratio (simplex.py:204-215)
+            bool okr;
+            const double a = current(A, t, check_row, C, A.T[check_row * A.ld + C]);
+            const double qr = row_ratio(a, A.col0[check_row], A.tol, okr);
+            if (a == 0.0) ctl->status = LP_ZERO_PIVOT;
+            else if (!(g < INFINITY) || !okr || !(qr <= tie_band(g, A.tol.ratio_tie)))
+                ctl->status = LP_BAD_PIVOT;
+        }
+        st_sc1(&ctl->ticket, 0u);
     }
 }
 
 // ---------------------------------------------------------------------------
-// K2s (sharded): after allreduce-min of the ratio, each rank offers its first
-// row within the global tie band (or the requested row) in its exchange slot.
-// Every block recomputes the (cheap) candidate and copies a slice of the row.
+// K1s (sharded): after the allreduce-min of the ratio, each rank offers its
+// first row within the global tie band (or the requested row) in its slot,
+// as CURRENT values.  Every block recomputes the (cheap) candidate and copies
+// a slice of the row.
 // ---------------------------------------------------------------------------
 
-__global__ void __launch_bounds__(256) k_pick(Args A, int mode)
+template <int TP>
+__global__ void __launch_bounds__(256) k_pick(Args A, int t, int mode)
 {
     __shared__ long long sl[16];
     Ctl *ctl = A.ctl;
@@ -303,20 +462,20 @@ __global__ void __launch_bounds__(256) k_pick(Args A, int mode)
     if (mode == PICK_RATIO) {
         const double g = *A.xg;
         if (!(g < INFINITY)) {
-            // every rank sees the same global minimum: unbounded everywhere
+            // every rank holds the same global minimum: unbounded everywhere
             if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_UNBOUNDED;
             return;
         }
-        const long long w = pick_from_records(A, C, g, sl);
+        const long long w = pick_from_records(A, t, C, g, sl);
         li = (w == NONE) ? -1 : w;
     } else {
         li = local_of(A, ctl->r);
         if (li >= 0 && mode == PICK_CHECK) {
-            const double *t = A.T + li * A.ld;
             bool okr;
             const double g = *A.xg;
-            const double qr = row_ratio(t[C], t[0], A.tol, okr);
-            if (t[C] == 0.0) code = LP_ZERO_PIVOT;
+            const double a = current(A, t, li, C, A.T[li * A.ld + C]);
+            const double qr = row_ratio(a, A.col0[li], A.tol, okr);
+            if (a == 0.0) code = LP_ZERO_PIVOT;
             else if (!(g < INFINITY) || !okr || !(qr <= tie_band(g, A.tol.ratio_tie)))
                 code = LP_BAD_PIVOT;
         }
@@ -326,142 +485,225 @@ __global__ void __launch_bounds__(256) k_pick(Args A, int mode)
         A.xs[1] = as_d(code);
     }
     if (li < 0) return;
-    const double *src = A.T + li * A.ld;
     for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < A.ld;
          j += (long long)gridDim.x * blockDim.x)
-        A.xs[SLOT_HDR + j] = src[j];
+        A.xs[SLOT_HDR + j] = current_row<TP>(A, t, li, j, A.T[li * A.ld + j]);
 }
 
-// ---------------------------------------------------------------------------
-// K2': explicit pivot (Tableau.pivot): multiplier snapshot only
-// ---------------------------------------------------------------------------
-
-__global__ void k_gather(Args A)
+// explicit pivot (Tableau.pivot): multiplier snapshot of the (current) column
+__global__ void k_gather(Args A, int t)
 {
     Ctl *ctl = A.ctl;
     if (ctl->status != LP_PIVOTED) return;
     const long long C = ctl->c + 1;
     for (long long li = blockIdx.x * (long long)blockDim.x + threadIdx.x; li < A.rows;
          li += (long long)gridDim.x * blockDim.x)
-        A.mult[li] = A.T[li * A.ld + C];
+        A.M[li * BMAX + t] = li == 0 ? A.row0[C] : current(A, t, li, C, A.T[li * A.ld + C]);
 }
 
 // ---------------------------------------------------------------------------
-// K3: normalised pivot row P = T[R] / a_RC, P[C] = 1   (tableau.py:300-302)
+// K2: leaving row (from the ratio summaries, the caller or the rank slots);
+// pivot row P[t] = current row R / a, P[t][C] = 1 (tableau.py:300-302);
+// pivot t applied to the current row 0 and column 0; per-block row-0
+// summaries; block 0 records the pivot (log, counters, stall test).
 // ---------------------------------------------------------------------------
 
-__device__ void finish_pivot_bookkeeping(const Args &A, Ctl *ctl)
+template <int TP>
+__global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, int rsrc, int peek)
 {
-    const long long k = ctl->npiv;
-    if (k < A.logcap) {
-        A.log[2 * k] = ctl->r;
-        A.log[2 * k + 1] = ctl->c;
-    }
-    ctl->npiv = k + 1;
-    if (ctl->mode == MODE_SOLVE && ctl->rule == LP_RULE_STANDARD) ctl->nstd += 1;
-}
-
-__global__ void k_prow(Args A)
-{
+    __shared__ double sd[16];
+    __shared__ long long sl[16];
+    __shared__ double s_q;
     Ctl *ctl = A.ctl;
     if (ctl->status != LP_PIVOTED) return;
-    const long long R = local_of(A, ctl->r);
     const long long C = ctl->c + 1;
-    const double *t = A.T + R * A.ld;
-    const double a = t[C];
+    long long R, rglob;
+    double a;
+    const double *src = nullptr;   // sharded: the current pivot row from its owner
+    if (rsrc == RSRC_SLOTS) {
+        const long long slot = SLOT_HDR + A.ld;
+        long long best = NONE, code = 0;
+        int who = -1;
+        for (int k = 0; k < A.nranks; ++k) {
+            const long long idx = as_ll(A.xr[k * slot]);
+            const long long cd = as_ll(A.xr[k * slot + 1]);
+            if (cd != 0) code = cd;
+            if (idx < best) { best = idx; who = k; }
+        }
+        if (code != 0 || best == NONE) {
+            if (blockIdx.x == 0 && threadIdx.x == 0)
+                ctl->status = code != 0 ? (int)code : LP_UNBOUNDED;
+            return;
+        }
+        if (peek) {   // findPivot*(False): report the row only
+            if (blockIdx.x == 0 && threadIdx.x == 0) ctl->r = best;
+            return;
+        }
+        src = A.xr + who * slot + SLOT_HDR;
+        rglob = best;
+        R = local_of(A, best);
+        a = src[C];
+    } else {
+        if (rsrc == RSRC_RECORDS) {
+            const double g = records_min(A, sd);
+            if (!(g < INFINITY)) {
+                if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_UNBOUNDED;
+                return;
+            }
+            R = pick_from_records(A, t, C, g, sl);
+        } else {
+            R = A.dR[t];
+        }
+        rglob = R - 1 + A.rb;
+        if (peek) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) ctl->r = rglob;
+            return;
+        }
+        a = A.M[R * BMAX + t];
+    }
     if (a == 0.0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_ZERO_PIVOT;
         return;
     }
-    for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < A.ld;
-         j += (long long)gridDim.x * blockDim.x)
-        A.P[j] = (j == C) ? 1.0 : t[j] / a;
-    if (blockIdx.x == 0 && threadIdx.x == 0) finish_pivot_bookkeeping(A, ctl);
-}
-
-// sharded: choose the lowest offered row among the gathered slots, normalise it
-__global__ void k_prow_sharded(Args A)
-{
-    Ctl *ctl = A.ctl;
-    if (ctl->status != LP_PIVOTED) return;
-    const long long slot = SLOT_HDR + A.ld;
-    long long best = NONE;
-    int who = -1;
-    long long code = 0;
-    for (int k = 0; k < A.nranks; ++k) {
-        const long long idx = as_ll(A.xr[k * slot]);
-        const long long cd = as_ll(A.xr[k * slot + 1]);
-        if (cd != 0) code = cd;
-        if (idx < best) { best = idx; who = k; }
+    const double f0 = A.M[t];            // row 0's multiplier (its current value at C)
+    const long long j = blockIdx.x * (long long)PROW_THREADS + threadIdx.x;
+    double v = INFINITY;
+    if (j < A.ld) {
+        const double x = src ? src[j] : current_row<TP>(A, t, R, j, A.T[R * A.ld + j]);
+        const double p = (j == C) ? 1.0 : x / a;
+        A.P[t * A.ld + j] = p;
+        v = upd(0, -1, f0, p, A.row0[j]);
+        A.row0[j] = v;
+        if (j == 0) A.col0[0] = v;
     }
-    if (code != 0 || best == NONE) {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            ctl->status = code != 0 ? (int)code : LP_UNBOUNDED;
-        return;
+    // column 0 of the local constraint rows (column 0 is never the pivot column)
+    {
+        const double x0 = src ? src[0] : current_row<TP>(A, t, R, 0, A.T[R * A.ld]);
+        const double p0 = x0 / a;
+        const long long stride = (long long)gridDim.x * blockDim.x;
+        for (long long li = 1 + blockIdx.x * (long long)blockDim.x + threadIdx.x; li < A.rows;
+             li += stride)
+            A.col0[li] = upd(li, R, A.M[li * BMAX + t], p0, A.col0[li]);
     }
-    const long long C = ctl->c + 1;
-    const double *t = A.xr + who * slot + SLOT_HDR;
-    const double a = t[C];
-    if (a == 0.0) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_ZERO_PIVOT;
-        return;
+    // entering-column summary of this slice of the new row 0
+    const bool cand = j >= 1 && j <= A.n;
+    const double lb = block_min(cand ? v : INFINITY, sd);
+    const long long ib =
+        block_min_ll(cand && lb < INFINITY && v <= tie_band(lb, A.tol.cost_tie) ? j : NONE, sl);
+    const long long fn = block_min_ll(cand && v < -A.tol.cost ? j : NONE, sl);
+    if (threadIdx.x == 0) s_q = 0.0;
+    __syncthreads();
+    if (ib != NONE && j == ib) s_q = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        A.erec[blockIdx.x].l = lb;
+        A.erec[blockIdx.x].i = ib;
+        A.erec[blockIdx.x].q = s_q;
+        A.erec[blockIdx.x].fneg = fn;
     }
-    for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < A.ld;
-         j += (long long)gridDim.x * blockDim.x)
-        A.P[j] = (j == C) ? 1.0 : t[j] / a;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctl->r = best;
-        finish_pivot_bookkeeping(A, ctl);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // j == 0: v is the new row0[0]
+        A.dR[t] = R;
+        A.dC[t] = C;
+        ctl->r = rglob;
+        const long long k = ctl->npiv;
+        if (k < A.logcap) {
+            A.log[2 * k] = rglob;
+            A.log[2 * k + 1] = C - 1;
+        }
+        ctl->npiv = k + 1;
+        ctl->ndef[grp] = t + 1;
+        if (ctl->mode == MODE_SOLVE && ctl->rule == LP_RULE_STANDARD) {
+            ctl->nstd += 1;
+            // stall bookkeeping (simplex.py:132-137) and the switch to the
+            // min-index rule (simplex.py:123,138)
+            const double z = -v;
+            const double z0 = ctl->z0;
+            if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) ctl->stuck += 1;
+            else ctl->stuck = 0;
+            if (ctl->stuck >= A.m + A.n) ctl->rule = LP_RULE_MIN_INDEX;
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
-// K4: rank-1 elimination, in place.
-//   Tile = 128 columns (one wave: 64 lanes x 16 B) x UPD_ROWS rows; the four
-//   waves of a block take interleaved rows of the tile.  Each lane keeps its
-//   two P values in registers for all its rows; per row the multiplier is a
-//   wave-uniform scalar load.  Rows with a zero multiplier are skipped
-//   (tableau.py:272), the pivot row is overwritten with P, the pivot column
-//   becomes the exact unit vector.
+// K3: the sweep.  T <- T with the group's deferred pivots 0..ndef-1 applied.
+//   Tile = 128 columns (one wave: 64 lanes x 16 B) x SWEEP_ROWS rows; the
+//   four waves of a block take interleaved rows.  Each lane keeps its slice
+//   of the ND deferred pivot rows in registers; a row's ND multipliers are one
+//   scalar load (M is row-major), so every row-level test is a scalar branch
+//   and the inner loop is just two FMAs per deferred pivot.  Tiles that hold
+//   one of the (at most ND) pivot rows take the general path.  Each element
+//   is loaded once and stored once.
 // ---------------------------------------------------------------------------
 
-__global__ void __launch_bounds__(256) k_update(Args A)
+template <int ND>
+__global__ void __launch_bounds__(256)
+k_sweep(double *__restrict__ T, const double *__restrict__ P, const double *__restrict__ M,
+        const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld,
+        long long rows, int grp)
 {
-    const Ctl *ctl = A.ctl;
-    if (ctl->status != LP_PIVOTED) return;
-    const long long R = local_of(A, ctl->r);   // -1 on a non-owner rank
-    const long long C = ctl->c + 1;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nd = (int)ctl->ndef[grp];     // <= ND
+    if (nd == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long j0 = (long long)blockIdx.x * 128 + lane * 2;
-    if (j0 >= A.ld) return;
-    const double2 p = *reinterpret_cast<const double2 *>(A.P + j0);
-    const bool c0 = (j0 == C), c1 = (j0 + 1 == C);
-    const long long rbeg = (long long)blockIdx.y * UPD_ROWS + wave;
-    const long long rend = min((long long)(blockIdx.y + 1) * UPD_ROWS, A.rows);
-    double *base = A.T + j0;
-    for (long long i = rbeg; i < rend; i += 4 * UPD_UNROLL) {
-        double2 x[UPD_UNROLL];
-        double f[UPD_UNROLL];
+    const long long r0 = (long long)blockIdx.y * SWEEP_ROWS;
+    const long long rend = min(r0 + SWEEP_ROWS, rows);
+    const bool active = j0 < ld;
+    // pivots s >= nd are padded as f = +0, P = +0: fma(-0, +0, y) == y exactly
+    double2 p[ND];
+    bool pivrow_here = false;
 #pragma unroll
-        for (int u = 0; u < UPD_UNROLL; ++u) {
-            const long long ii = i + 4 * u;
-            f[u] = (ii < rend) ? A.mult[ii] : 0.0;
-            if (ii < rend && ii != R && f[u] != 0.0)
-                x[u] = *reinterpret_cast<const double2 *>(base + ii * A.ld);
+    for (int s = 0; s < ND; ++s) {
+        p[s] = make_double2(0.0, 0.0);
+        if (s < nd) {
+            if (active) p[s] = *reinterpret_cast<const double2 *>(P + s * ld + j0);
+            const long long R = dR[s];
+            pivrow_here |= (R >= r0 && R < rend);
+        }
+    }
+    if (!active) return;
+    double *base = T + j0;
+    for (long long i = r0 + wave; i < rend; i += 4 * SWEEP_UNROLL) {
+        // rows past the tile end re-load the last row (in bounds) and are not stored
+        double2 x[SWEEP_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SWEEP_UNROLL; ++u) {
+            const long long ii = min(i + 4 * u, rend - 1);
+            x[u] = *reinterpret_cast<const double2 *>(base + ii * ld);
         }
 #pragma unroll
-        for (int u = 0; u < UPD_UNROLL; ++u) {
+        for (int u = 0; u < SWEEP_UNROLL; ++u) {
             const long long ii = i + 4 * u;
-            if (ii >= rend) continue;
-            double2 *dst = reinterpret_cast<double2 *>(base + ii * A.ld);
-            if (ii == R) {
-                *dst = p;
-            } else if (f[u] != 0.0) {
-                double2 y;
-                y.x = c0 ? 0.0 : fma(-f[u], p.x, x[u].x);
-                y.y = c1 ? 0.0 : fma(-f[u], p.y, x[u].y);
-                *dst = y;
+            if (ii >= rend) break;
+            double fr[ND];                      // one wide scalar load per row
+            const double *f = M + ii * BMAX;
+#pragma unroll
+            for (int s = 0; s < ND; ++s) {
+                const double v = f[s];
+                fr[s] = s < nd ? v : 0.0;
             }
+            double2 y = x[u];
+            if (!pivrow_here) {
+#pragma unroll
+                for (int s = 0; s < ND; ++s) {
+                    y.x = fma(-fr[s], p[s].x, y.x);
+                    y.y = fma(-fr[s], p[s].y, y.y);
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < ND; ++s) {
+                    if (s < nd) {
+                        if (ii == dR[s]) {
+                            y = p[s];
+                        } else {
+                            y.x = fma(-fr[s], p[s].x, y.x);
+                            y.y = fma(-fr[s], p[s].y, y.y);
+                        }
+                    }
+                }
+            }
+            *reinterpret_cast<double2 *>(base + ii * ld) = y;
         }
     }
 }
@@ -478,12 +720,36 @@ __global__ void k_group_min(double *const *ptrs, int n)
 // launch wrappers
 // ---------------------------------------------------------------------------
 
-int ratio_blocks(long long rows) { return (int)((rows - 1 + RATIO_CHUNK - 1) / RATIO_CHUNK); }
 
-hipError_t launch_reset(hipStream_t s, Ctl *ctl, int mode, int rule, long long cap, long long r,
-                        long long c, const double *T)
+// compile-time bound of the deferred-pivot count: 0, 1, 2, 4, 8, 16, 32
+static int bound_of(int t)
 {
-    hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, s, ctl, mode, rule, cap, r, c, T);
+    return t <= 0 ? 0 : t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : t <= 8 ? 8 : t <= 16 ? 16 : 32;
+}
+
+#define TP_DISPATCH(t, KERNEL, ...)                                                           \
+    switch (bound_of(t)) {                                                                     \
+    case 0: hipLaunchKernelGGL(KERNEL<0>, __VA_ARGS__); break;                                 \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                                 \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                                 \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                                 \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                                 \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                               \
+    default: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                               \
+    }
+
+hipError_t launch_reset(hipStream_t s, const Args &A, int mode, int rule, int chain, long long cap,
+                        long long r, long long c)
+{
+    hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, s, A, mode, rule, chain, cap, r, c);
+    return hipGetLastError();
+}
+
+hipError_t launch_load_eager(hipStream_t s, const Args &A)
+{
+    const long long w = A.ld > A.rows ? A.ld : A.rows;
+    const long long g = (w + 255) / 256;
+    hipLaunchKernelGGL(k_load_eager, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, A);
     return hipGetLastError();
 }
 
@@ -493,45 +759,57 @@ hipError_t launch_enter(hipStream_t s, const Args &A)
     return hipGetLastError();
 }
 
-hipError_t launch_ratio(hipStream_t s, const Args &A, int mode, long long check_local_row)
+hipError_t launch_ratio(hipStream_t s, const Args &A, int t, int grp, int mode, int from_erec,
+                        long long check_local_row)
 {
     const int g = ratio_blocks(A.rows);
-    if (g <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ratio, dim3(g), dim3(RATIO_THREADS), 0, s, A, mode, check_local_row);
+    if (g <= 0 || t < 0 || t >= BMAX) return hipErrorInvalidValue;
+    TP_DISPATCH(t, k_ratio, dim3(g), dim3(RATIO_THREADS), 0, s, A, t, grp, mode, from_erec,
+                check_local_row)
     return hipGetLastError();
 }
 
-static unsigned row_blocks(long long ld) { return (unsigned)((ld + 255) / 256); }
-
-hipError_t launch_pick(hipStream_t s, const Args &A, int mode)
+hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode)
 {
-    hipLaunchKernelGGL(k_pick, dim3(row_blocks(A.ld)), dim3(256), 0, s, A, mode);
+    if (t < 0 || t >= BMAX) return hipErrorInvalidValue;
+    TP_DISPATCH(t, k_pick, dim3(prow_blocks(A.ld)), dim3(256), 0, s, A, t, mode)
     return hipGetLastError();
 }
 
-hipError_t launch_gather(hipStream_t s, const Args &A)
+hipError_t launch_gather(hipStream_t s, const Args &A, int t)
 {
     const long long g = (A.rows + 255) / 256;
-    hipLaunchKernelGGL(k_gather, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_gather, dim3((unsigned)(g < 1024 ? g : 1024)), dim3(256), 0, s, A, t);
     return hipGetLastError();
 }
 
-hipError_t launch_prow(hipStream_t s, const Args &A)
+hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek)
 {
-    hipLaunchKernelGGL(k_prow, dim3(row_blocks(A.ld)), dim3(256), 0, s, A);
+    if (t < 0 || t >= BMAX) return hipErrorInvalidValue;
+    TP_DISPATCH(t, k_prow, dim3(prow_blocks(A.ld)), dim3(PROW_THREADS), 0, s, A, t, grp, rsrc,
+                peek)
     return hipGetLastError();
 }
 
-hipError_t launch_prow_sharded(hipStream_t s, const Args &A)
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max)
 {
-    hipLaunchKernelGGL(k_prow_sharded, dim3(row_blocks(A.ld)), dim3(256), 0, s, A);
-    return hipGetLastError();
-}
-
-hipError_t launch_update(hipStream_t s, const Args &A)
-{
-    const dim3 grid((unsigned)((A.ld + 127) / 128), (unsigned)((A.rows + UPD_ROWS - 1) / UPD_ROWS));
-    hipLaunchKernelGGL(k_update, grid, dim3(256), 0, s, A);
+    const dim3 grid((unsigned)((A.ld + 127) / 128),
+                    (unsigned)((A.rows + SWEEP_ROWS - 1) / SWEEP_ROWS));
+#define SWEEP_CASE(N)                                                                        \
+    case N:                                                                                  \
+        hipLaunchKernelGGL(k_sweep<N>, grid, dim3(256), 0, s, A.T, A.P, A.M, A.dR, A.ctl,   \
+                           A.ld, A.rows, grp);                                               \
+        break;
+    switch (bound_of(nd_max < 1 ? 1 : nd_max)) {
+        SWEEP_CASE(1)
+        SWEEP_CASE(2)
+        SWEEP_CASE(4)
+        SWEEP_CASE(8)
+        SWEEP_CASE(16)
+        default:
+        SWEEP_CASE(32)
+    }
+#undef SWEEP_CASE
     return hipGetLastError();
 }
 

@@ -37,7 +37,11 @@ struct lp_handle {
     int64_t m = 0, n = 0, ld = 0;   // global problem
     int64_t rb = 0, rc = 0;         // local constraint block [rb, rb+rc)
     int64_t rows = 0;               // local rows = rc + 1
-    double *T = nullptr, *P = nullptr, *mult = nullptr;
+    double *T = nullptr, *P = nullptr, *M = nullptr, *row0 = nullptr, *col0 = nullptr;
+    long long *dR = nullptr, *dC = nullptr;
+    lpk::ERec *erec = nullptr;
+    int block = 8;                  // pivots deferred into one sweep (1..BMAX)
+    bool eager_ok = false;          // row0/col0 mirror the stored tableau
     Ctl *ctl = nullptr;
     Ctl *hctl = nullptr;            // pinned mirror
     long long *log = nullptr;
@@ -161,11 +165,16 @@ static Args args_of(const lp_handle *h)
 {
     Args A;
     A.T = h->T;
+    A.row0 = h->row0;
+    A.col0 = h->col0;
+    A.M = h->M;
     A.P = h->P;
-    A.mult = h->mult;
+    A.dR = h->dR;
+    A.dC = h->dC;
     A.ctl = h->ctl;
     A.log = h->log;
     A.rec = h->rec;
+    A.erec = h->erec;
     A.xg = h->xg;
     A.xs = h->xs;
     A.xr = h->xr;
@@ -219,9 +228,18 @@ static int alloc_handle(lp_handle *h)
     const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
     HCHK(h, hipMalloc(&h->T, tbytes));
     HCHK(h, hipMemsetAsync(h->T, 0, tbytes, h->s));
-    HCHK(h, hipMalloc(&h->P, (size_t)h->ld * sizeof(double)));
-    HCHK(h, hipMemsetAsync(h->P, 0, (size_t)h->ld * sizeof(double), h->s));
-    HCHK(h, hipMalloc(&h->mult, (size_t)h->rows * sizeof(double)));
+    HCHK(h, hipMalloc(&h->P, (size_t)lpk::BMAX * h->ld * sizeof(double)));
+    HCHK(h, hipMemsetAsync(h->P, 0, (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
+    HCHK(h, hipMalloc(&h->M, (size_t)lpk::BMAX * h->rows * sizeof(double)));
+    HCHK(h, hipMemsetAsync(h->M, 0, (size_t)lpk::BMAX * h->rows * sizeof(double), h->s));
+    HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));
+    HCHK(h, hipMemsetAsync(h->row0, 0, (size_t)h->ld * sizeof(double), h->s));
+    HCHK(h, hipMalloc(&h->col0, (size_t)h->rows * sizeof(double)));
+    HCHK(h, hipMemsetAsync(h->col0, 0, (size_t)h->rows * sizeof(double), h->s));
+    HCHK(h, hipMalloc(&h->dR, (size_t)lpk::BMAX * sizeof(long long)));
+    HCHK(h, hipMalloc(&h->dC, (size_t)lpk::BMAX * sizeof(long long)));
+    HCHK(h, hipMalloc(&h->erec, (size_t)std::max(1, lpk::prow_blocks(h->ld)) * sizeof(lpk::ERec)));
+    h->eager_ok = true;   // all zero
     HCHK(h, hipMalloc(&h->ctl, sizeof(Ctl)));
     HCHK(h, hipMemsetAsync(h->ctl, 0, sizeof(Ctl), h->s));
     HCHK(h, hipHostMalloc(&h->hctl, sizeof(Ctl), hipHostMallocDefault));
@@ -230,6 +248,7 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMalloc(&h->log, (size_t)h->logcap * 2 * sizeof(long long)));
     const int nrec = std::max(1, lpk::ratio_blocks(h->rows));
     HCHK(h, hipMalloc(&h->rec, (size_t)nrec * sizeof(Rec)));
+    HCHK(h, hipMemsetAsync(h->rec, 0, (size_t)nrec * sizeof(Rec), h->s));
     if (h->nranks > 1 || h->comm) {
         HCHK(h, hipMalloc(&h->xg, sizeof(double)));
         HCHK(h, hipMalloc(&h->xs, (size_t)slot_len(h) * sizeof(double)));
@@ -370,7 +389,12 @@ extern "C" int lp_destroy(lp_handle *h)
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->T) (void)hipFree(h->T);
     if (h->P) (void)hipFree(h->P);
-    if (h->mult) (void)hipFree(h->mult);
+    if (h->M) (void)hipFree(h->M);
+    if (h->row0) (void)hipFree(h->row0);
+    if (h->col0) (void)hipFree(h->col0);
+    if (h->dR) (void)hipFree(h->dR);
+    if (h->dC) (void)hipFree(h->dC);
+    if (h->erec) (void)hipFree(h->erec);
     if (h->ctl) (void)hipFree(h->ctl);
     if (h->hctl) (void)hipHostFree(h->hctl);
     if (h->log) (void)hipFree(h->log);
@@ -452,7 +476,23 @@ static int transfer_rows(lp_handle *h, int64_t row0, int64_t nrows, double *buf,
 extern "C" int lp_upload_rows(lp_handle *h, int64_t row0, int64_t nrows, const double *src,
                               int64_t ldh)
 {
+    h->eager_ok = false;
     return transfer_rows<true>(h, row0, nrows, const_cast<double *>(src), ldh);
+}
+
+extern "C" int lp_set_block(lp_handle *h, int pivots_per_sweep)
+{
+    if (pivots_per_sweep < 1 || pivots_per_sweep > lpk::BMAX)
+        return fail(h, LP_BAD_ARG, "pivots_per_sweep must be in [1, 32]");
+    for (lp_handle *x : members_of(h))
+        if (x) x->block = pivots_per_sweep;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_get_block(const lp_handle *h, int *pivots_per_sweep)
+{
+    *pivots_per_sweep = h->block;
+    return LP_PIVOTED;
 }
 
 extern "C" int lp_download_rows(lp_handle *h, int64_t row0, int64_t nrows, double *dst,
@@ -481,10 +521,10 @@ static int ensure_log(lp_handle *h, int64_t need)
     return LP_PIVOTED;
 }
 
-static int launch_update_timed(lp_handle *h, const Args &A)
+static int launch_sweep_timed(lp_handle *h, const Args &A, int grp)
 {
     if (!h->prof) {
-        HCHK(h, lpk::launch_update(h->s, A));
+        HCHK(h, lpk::launch_sweep(h->s, A, grp, h->block));
         return LP_PIVOTED;
     }
     if (h->evused + 2 > h->ev.size()) {
@@ -495,13 +535,13 @@ static int launch_update_timed(lp_handle *h, const Args &A)
         h->ev.push_back(b);
     }
     HCHK(h, hipEventRecord(h->ev[h->evused], h->s));
-    HCHK(h, lpk::launch_update(h->s, A));
+    HCHK(h, lpk::launch_sweep(h->s, A, grp, h->block));
     HCHK(h, hipEventRecord(h->ev[h->evused + 1], h->s));
     h->evused += 2;
     return LP_PIVOTED;
 }
 
-// after a stream sync: fold recorded update launches into the totals
+// after a stream sync: fold recorded sweep launches into the totals
 static int collect_profile(lp_handle *h)
 {
     for (size_t k = 0; k + 1 < h->evused; k += 2) {
@@ -534,47 +574,59 @@ static std::vector<Args> args_all(const Members &M)
     return v;
 }
 
-// Everything after the entering scan of one pivot.  sel: 0 = ratio test,
-// 1 = validated row (Simplex.pivot), 2 = explicit row (Tableau.pivot).
-// do_update=false stops after the pivot row is known (findPivot*(False)).
-static int enqueue_tail(const Members &M, const std::vector<Args> &A, int sel, bool do_update)
+// Leaving-row choice + pivot row of pivot t of group grp.
+// sel: 0 = ratio test, 1 = validated row (Simplex.pivot), 2 = explicit row
+// (Tableau.pivot).  from_erec: the entering column comes from the previous
+// pivot's row-0 summaries (chained pivots).  peek: stop once the leaving row
+// is known (findPivot*(False)).
+static int enqueue_select(const Members &M, const std::vector<Args> &A, int t, int grp, int sel,
+                          int from_erec, bool peek)
 {
     lp_handle *h0 = M[0];
     if (!h0->comm) {
-        if (sel == 0) HCHK(h0, lpk::launch_ratio(h0->s, A[0], lpk::RATIO_FULL, -1));
-        else if (sel == 1)
-            HCHK(h0, lpk::launch_ratio(h0->s, A[0], lpk::RATIO_CHECK,
-                                       local_row(h0, h0->hctl->r + 1)));
-        else HCHK(h0, lpk::launch_gather(h0->s, A[0]));
-        if (!do_update) return LP_PIVOTED;
-        HCHK(h0, lpk::launch_prow(h0->s, A[0]));
-        return launch_update_timed(h0, A[0]);
+        if (sel == 0) {
+            HCHK(h0, lpk::launch_ratio(h0->s, A[0], t, grp, lpk::RATIO_FULL, from_erec, -1));
+            HCHK(h0, lpk::launch_prow(h0->s, A[0], t, grp, lpk::RSRC_RECORDS, peek));
+        } else {
+            if (sel == 1)
+                HCHK(h0, lpk::launch_ratio(h0->s, A[0], t, grp, lpk::RATIO_CHECK, 0,
+                                           local_row(h0, h0->hctl->r + 1)));
+            else HCHK(h0, lpk::launch_gather(h0->s, A[0], t));
+            HCHK(h0, lpk::launch_prow(h0->s, A[0], t, grp, lpk::RSRC_GIVEN, 0));
+        }
+        return LP_PIVOTED;
     }
     for (size_t k = 0; k < M.size(); ++k) {
-        if (sel == 2) HCHK(M[k], lpk::launch_gather(M[k]->s, A[k]));
-        else HCHK(M[k], lpk::launch_ratio(M[k]->s, A[k], lpk::RATIO_LOCAL, -1));
+        if (sel == 2) HCHK(M[k], lpk::launch_gather(M[k]->s, A[k], t));
+        else HCHK(M[k], lpk::launch_ratio(M[k]->s, A[k], t, grp, lpk::RATIO_LOCAL, from_erec, -1));
     }
     if (sel != 2) CALL(h0->comm->allreduce_min(M));
     const int pm = sel == 0 ? lpk::PICK_RATIO : sel == 1 ? lpk::PICK_CHECK : lpk::PICK_EXPLICIT;
-    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_pick(M[k]->s, A[k], pm));
+    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_pick(M[k]->s, A[k], t, pm));
     CALL(h0->comm->allgather(M));
-    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_prow_sharded(M[k]->s, A[k]));
-    if (!do_update) return LP_PIVOTED;
-    for (size_t k = 0; k < M.size(); ++k) CALL(launch_update_timed(M[k], A[k]));
+    for (size_t k = 0; k < M.size(); ++k)
+        HCHK(M[k], lpk::launch_prow(M[k]->s, A[k], t, grp, lpk::RSRC_SLOTS, peek));
     return LP_PIVOTED;
 }
 
-static int enqueue_pivot(const Members &M, const std::vector<Args> &A)
+static int enqueue_sweep(const Members &M, const std::vector<Args> &A, int grp)
 {
-    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
-    return enqueue_tail(M, A, 0, true);
+    for (size_t k = 0; k < M.size(); ++k) CALL(launch_sweep_timed(M[k], A[k], grp));
+    return LP_PIVOTED;
 }
 
-static int reset_all(const Members &M, int mode, int rule, int64_t cap, int64_t r, int64_t c)
+// every call starts here: eager row 0 / column 0 current, control reset
+static int begin_call(const Members &M, const std::vector<Args> &A, int mode, int rule, int chain,
+                      int64_t cap, int64_t r, int64_t c)
 {
-    for (lp_handle *h : M) {
+    for (size_t k = 0; k < M.size(); ++k) {
+        lp_handle *h = M[k];
         HCHK(h, hipSetDevice(h->dev));
-        HCHK(h, lpk::launch_reset(h->s, h->ctl, mode, rule, cap, r, c, h->T));
+        if (!h->eager_ok) {
+            HCHK(h, lpk::launch_load_eager(h->s, A[k]));
+            h->eager_ok = true;
+        }
+        HCHK(h, lpk::launch_reset(h->s, A[k], mode, rule, chain, cap, r, c));
         h->hctl->r = r;
         h->hctl->c = c;
     }
@@ -582,26 +634,40 @@ static int reset_all(const Members &M, int mode, int rule, int64_t cap, int64_t 
 }
 
 // Runs pivots until the device reports a status other than LP_PIVOTED or
-// `limit` pivots have been enqueued (limit < 0: unlimited).  Batch sizes are
-// a deterministic sequence, so every rank of a sharded job enqueues the same
+// `limit` pivots have been enqueued (limit < 0: unlimited).  Pivots are
+// enqueued in groups of `block` followed by one sweep; the host knows each
+// pivot's index t in its group and the group parity.  Batch sizes are a
+// deterministic sequence, so every rank of a sharded job enqueues the same
 // collectives in the same order.
 static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t limit)
 {
     const Members M = members_of(h);
-    CALL(reset_all(M, mode, rule, cap, -1, -1));
+    std::vector<Args> A = args_all(M);
+    CALL(begin_call(M, A, mode, rule, 1, cap, -1, -1));
+    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
+    const int B = h->block;
     int64_t enq = 0;
-    int64_t batch = 8;
+    int64_t batch = 8 * B;
+    int grp = 0;
     for (;;) {
         int64_t b = batch;
         if (limit >= 0) b = std::min(b, limit - enq);
         for (lp_handle *x : M) CALL(ensure_log(x, enq + b));
-        const std::vector<Args> A = args_all(M);
-        for (int64_t k = 0; k < b; ++k) CALL(enqueue_pivot(M, A));
+        A = args_all(M);
+        int t = 0;
+        for (int64_t k = 0; k < b; ++k) {
+            CALL(enqueue_select(M, A, t, grp, 0, enq + k > 0 ? 1 : 0, false));
+            if (++t == B || k + 1 == b) {
+                CALL(enqueue_sweep(M, A, grp));
+                grp ^= 1;
+                t = 0;
+            }
+        }
         enq += b;
         CALL(sync_ctl(M));
         if (h->hctl->status != LP_PIVOTED) return h->hctl->status;
         if (limit >= 0 && enq >= limit) return LP_PIVOTED;
-        batch = std::min<int64_t>(batch * 2, 1024);
+        batch = std::min<int64_t>(batch * 2, std::max<int64_t>(1024, 32 * B));
     }
 }
 
@@ -631,10 +697,11 @@ extern "C" int lp_find_pivot(lp_handle *h, int rule, int do_pivot, int64_t *r, i
     if (rule != LP_RULE_STANDARD && rule != LP_RULE_MIN_INDEX)
         return fail(h, LP_BAD_ARG, "unknown rule");
     const Members M = members_of(h);
-    CALL(reset_all(M, lpk::MODE_RUN, rule, -1, -1, -1));
     const std::vector<Args> A = args_all(M);
+    CALL(begin_call(M, A, lpk::MODE_RUN, rule, 0, -1, -1, -1));
     for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
-    CALL(enqueue_tail(M, A, 0, do_pivot != 0));
+    CALL(enqueue_select(M, A, 0, 0, 0, 0, do_pivot == 0));
+    if (do_pivot) CALL(enqueue_sweep(M, A, 0));
     CALL(sync_ctl(M));
     if (h->hctl->status == LP_PIVOTED) {
         *r = h->hctl->r;
@@ -648,9 +715,10 @@ static int explicit_pivot(lp_handle *h, int64_t r, int64_t c, bool checked)
     if (r < 0 || r >= h->m || c < 0 || c >= h->n)
         return fail(h, LP_BAD_ARG, "pivot index out of range");
     const Members M = members_of(h);
-    CALL(reset_all(M, lpk::MODE_RUN, LP_RULE_STANDARD, -1, r, c));
     const std::vector<Args> A = args_all(M);
-    CALL(enqueue_tail(M, A, checked ? 1 : 2, true));
+    CALL(begin_call(M, A, lpk::MODE_RUN, LP_RULE_STANDARD, 0, -1, r, c));
+    CALL(enqueue_select(M, A, 0, 0, checked ? 1 : 2, 0, false));
+    CALL(enqueue_sweep(M, A, 0));
     CALL(sync_ctl(M));
     return h->hctl->status;
 }

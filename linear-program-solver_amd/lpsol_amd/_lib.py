@@ -66,6 +66,8 @@ _PROTOS = {
     "lp_run": (C.c_int, [_H, C.c_int, _I64, _P64]),
     "lp_pivot_log": (C.c_int, [_H, _P64, _I64, _P64]),
     "lp_objective": (C.c_int, [_H, _PD]),
+    "lp_set_block": (C.c_int, [_H, C.c_int]),
+    "lp_get_block": (C.c_int, [_H, C.POINTER(C.c_int)]),
     "lp_profile": (C.c_int, [_H, C.c_int]),
     "lp_update_time": (C.c_int, [_H, _PD, _P64]),
     "lp_last_error": (C.c_char_p, [_H]),
@@ -247,6 +249,15 @@ class Engine:
             self._check(self.lib.lp_pivot_log(self.h, out.ctypes.data_as(_P64), cnt.value,
                                               C.byref(cnt)), self.h)
         return out
+
+    def set_block(self, pivots_per_sweep: int):
+        """pivots deferred into one sweep of the tableau (1..32)"""
+        self._check(self.lib.lp_set_block(self.h, int(pivots_per_sweep)), self.h)
+
+    def get_block(self) -> int:
+        b = C.c_int()
+        self.lib.lp_get_block(self.h, C.byref(b))
+        return b.value
 
     # -- timing -------------------------------------------------------------
     def profile(self, enable: bool):

@@ -17,9 +17,13 @@
  * Float semantics (the contract shared with linear-program-solver_amd/csrc):
  *   pivot(r,c): R=r+1, C=c+1, a=T[R][C] (a==0 -> ZERO_PIVOT)
  *     P[j] = T[R][j] / a (IEEE division), P[C] = 1
- *     for every row i != R with f = T[i][C] != 0:
- *         T[i][j] = fma(-f, P[j], T[i][j])  for j != C,   T[i][C] = 0
+ *     for every row i != R, f = T[i][C]:
+ *         T[i][j] = fma(-f, P[j], T[i][j])  for all j (at j = C this is exactly +0)
  *     T[R] = P
+ *   The reference skips rows whose multiplier is zero (tableau.py:272); in
+ *   float64 fma(-0, p, x) == x for every finite x (only the sign of a zero x
+ *   can differ), so rows are not skipped -- the branch-free form lets the
+ *   engine's deferred sweep be pure FMAs.
  *   entering, standard : g = min c_j; optimal unless g < -tol.cost;
  *                        c = first j with c_j <= g + tol.cost_tie*|g|
  *   entering, min-index: c = first j with c_j < -tol.cost
@@ -51,9 +55,7 @@ int lpf_pivot(double *T, int64_t m, int64_t n, int64_t ld, int64_t r, int64_t c)
         if (i == R) continue;
         double *t = row(T, ld, i);
         const double f = t[C];
-        if (f == 0.0) continue;
         for (int64_t j = 0; j <= n; ++j) t[j] = fma(-f, p[j], t[j]);
-        t[C] = 0.0;
     }
     return LP_PIVOTED;
 }

@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU-box session: each step has its own time limit; a test FAILURE
+# (exit 1) lets the next step run, anything else (fault, abort, timeout)
+# ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=$PWD/gpurun_out
+mkdir -p "$OUT"
+run() {
+    local name=$1 t=$2; shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -5 "$OUT/$name.log"
+    if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name"; exit "$rc"; fi
+}
+for step in "$@"; do
+    case "$step" in
+        pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 600 python bench.py ;;
+        benchq) run benchq 300 python bench.py --no-cpu-baseline ;;
+        bsweep)
+            for B in 1 2 4 8 16 32; do
+                run bench_b$B 300 python bench.py --no-cpu-baseline --block $B
+            done ;;
+        prof16)
+            export TMPDIR=/tmp
+            run rocprof16 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof16" -o run -- python3 "$PWD/bench.py" --steps 512 --block 16 --no-cpu-baseline ;;
+        prof)
+            export TMPDIR=/tmp
+            run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$PWD/bench.py" --steps 200 --no-cpu-baseline ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done

@@ -39,9 +39,16 @@ def _obj_ok(z, fx):
     return abs(z - obj) <= REL * max(1.0, abs(obj))
 
 
-def engine_of(T):
+def _initial_basis(T):
+    bc = [0] * (T.shape[0] - 1)
+    assert Tableau.fromArray(T).isCanonical(bc)
+    return bc
+
+
+def engine_of(T, block=8):
     e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
     e.upload(T)
+    e.set_block(block)
     return e
 
 
@@ -68,10 +75,11 @@ def test_reference_kat_pivot_pair():
 
 
 # ----------------------------------------------------------- golden solves
+@pytest.mark.parametrize("block", [1, 8])
 @pytest.mark.parametrize("fx", SMALL["solve"] + BIG["solve"], ids=_ids(SMALL["solve"] + BIG["solve"]))
-def test_solve_matches_reference(fx):
+def test_solve_matches_reference(fx, block):
     T = fixture_input(fx)
-    e = engine_of(T)
+    e = engine_of(T, block)
     st, npiv, nstd = e.solve()
     assert st == _lib.OPTIMAL
     assert e.log().tolist() == fx["seq"]
@@ -84,9 +92,10 @@ def test_solve_matches_reference(fx):
 
 @pytest.mark.parametrize("fx", SMALL["standard_k"] + BIG["standard_k"],
                          ids=_ids(SMALL["standard_k"] + BIG["standard_k"]))
-def test_standard_k_matches_reference(fx):
+@pytest.mark.parametrize("block", [1, 5, 32])
+def test_standard_k_matches_reference(fx, block):
     T = fixture_input(fx)
-    e = engine_of(T)
+    e = engine_of(T, block)
     st, done = e.run(_lib.RULE_STANDARD, fx["k"])
     assert e.log().tolist() == fx["seq"]
     assert (st == _lib.OPTIMAL) == (fx["end"] == "optimal")
@@ -115,7 +124,15 @@ def test_frontend_simplex_solve_bfs():
         s.solve()
         assert s.getBasicSequence() == fx["bfs"], fx["name"]
         assert _obj_ok(s.getObjValue(), fx)
-        assert sorted(j for j, mk in enumerate(t.getVarMarks()) if mk) == sorted(fx["bfs"])
+        # marks follow _pivot's bookkeeping only (simplex.py:192-197): a
+        # canonical start returns before any mark is set (simplex.py:46-47)
+        marks = [False] * t.getNumVars()
+        bfs = _initial_basis(fixture_input(fx))
+        for r, c in fx["seq"]:
+            marks[bfs[r]] = False
+            bfs[r] = c
+            marks[c] = True
+        assert t.getVarMarks() == marks
         bfs = s.getBFS()
         assert set(bfs) == set(fx["bfs"])
 
@@ -171,9 +188,10 @@ def test_optimal_at_start_and_cap():
     ("tall", 257, 64, 30), ("mixed", 300, 191, 30), ("tall", 513, 7, 20),
     ("tall", 1000, 2, 10), ("tall", 2, 5000, 10), ("mixed", 255, 129, 40),
 ])
-def test_ragged_shapes_bit_exact(kind, m, ns, k):
+@pytest.mark.parametrize("block", [1, 7, 32])
+def test_ragged_shapes_bit_exact(kind, m, ns, k, block):
     T = gen.tableau(kind, m, ns, 77)
-    e = engine_of(T)
+    e = engine_of(T, block)
     st, done = e.run(_lib.RULE_STANDARD, k)
     o = F64Tableau(T)
     ost, olog = o.run(0, k)
@@ -181,15 +199,16 @@ def test_ragged_shapes_bit_exact(kind, m, ns, k):
     assert np.array_equal(e.download(), o.T)
 
 
-def test_cfg3_full_size_bit_exact():
-    """4096 x 8192 (the 1-GPU roofline config): 12 standard pivots, whole
+@pytest.mark.parametrize("block", [1, 32])
+def test_cfg3_full_size_bit_exact(block):
+    """4096 x 8192 (the 1-GPU roofline config): 40 standard pivots, whole
     268 MB tableau bit-identical to the f64 oracle."""
     T = gen.tableau("mixed", 4096, 4096, 3)
-    e = engine_of(T)
-    st, done = e.run(_lib.RULE_STANDARD, 12)
-    assert st == _lib.PIVOTED and done == 12
+    e = engine_of(T, block)
+    st, done = e.run(_lib.RULE_STANDARD, 40)
+    assert st == _lib.PIVOTED and done == 40
     o = F64Tableau(T)
-    _, olog = o.run(0, 12)
+    _, olog = o.run(0, 40)
     assert e.log().tolist() == olog.tolist()
     D = e.download()
     assert np.array_equal(D, o.T)
@@ -200,8 +219,9 @@ def test_cfg3_full_size_bit_exact():
 
 
 # ------------------------------------------------------------ sharding
+@pytest.mark.parametrize("block", [1, 6])
 @pytest.mark.parametrize("nshards", [1, 2, 3, 5, 8])
-def test_sharded_group_invariance(nshards):
+def test_sharded_group_invariance(nshards, block):
     """Row-sharded protocol (allreduce-min + slot allgather) emulated in one
     process: identical sequence and bit-identical rows for any shard count."""
     T = gen.tableau("mixed", 300, 200, 9)
@@ -211,6 +231,7 @@ def test_sharded_group_invariance(nshards):
     grp = _lib.create_group(m, n, nshards)
     for g in grp:
         g.upload(T)
+    grp[0].set_block(block)
     st, npiv, nstd = grp[0].solve()
     assert (st, npiv, nstd) == (st0, npiv0, nstd0)
     assert grp[0].log().tolist() == ref.log().tolist()
@@ -260,10 +281,41 @@ def test_rccl_single_rank_communicator():
     assert np.array_equal(e.rows(0, m + 1), ref.download())
 
 
-def test_update_kernel_event_timing():
+def test_sweep_kernel_event_timing():
     T = gen.tableau("mixed", 512, 512, 7)
-    e = engine_of(T)
+    e = engine_of(T, 4)
     e.profile(True)
-    e.run(_lib.RULE_STANDARD, 6)
+    e.run(_lib.RULE_STANDARD, 10)      # sweeps after pivots 4, 8 and 10
     ms, n = e.update_time()
-    assert n == 6 and ms > 0
+    assert n == 3 and ms > 0
+
+
+def test_block_size_invariance():
+    """every deferral depth gives the same bits (the sweep replays the exact
+    per-pivot float64 operations)"""
+    T = gen.tableau("mixed", 200, 300, 5)
+    outs = []
+    for block in (1, 2, 3, 8, 13, 31, 32):
+        e = engine_of(T, block)
+        e.run(_lib.RULE_STANDARD, 70)
+        outs.append((e.log().tolist(), e.download()))
+    for log, D in outs[1:]:
+        assert log == outs[0][0]
+        assert np.array_equal(D, outs[0][1])
+
+
+def test_find_without_pivot_leaves_tableau_untouched():
+    T = gen.tableau("mixed", 64, 64, 8)
+    for grp in ([engine_of(T)], _lib.create_group(64, 128, 3)):
+        for g in grp:
+            g.upload(T)
+        o = F64Tableau(T)
+        assert grp[0].find(_lib.RULE_STANDARD, False) == o.find(0)
+        assert grp[0].find(_lib.RULE_MIN_INDEX, False) == o.find(1)
+        st, done = grp[0].run(_lib.RULE_STANDARD, 5)
+        o.run(0, 5)
+        for g in grp:
+            b, c = g.row_begin, g.row_count
+            assert np.array_equal(g.rows(1 + b, c), o.T[1 + b:1 + b + c])
+        for g in reversed(grp):
+            g.close()
