@@ -54,6 +54,9 @@ struct Ctl {
     double z0;           // obj_val at the start of solve (simplex.py:118)
     unsigned ticket;     // last-block ticket of k_ratio (LOCAL / CHECK modes)
     unsigned pad;
+    unsigned bar[2];     // grid-barrier counters of k_group (by group parity)
+    unsigned bar_timeout;// set if a k_group barrier gave up (never expected)
+    unsigned pad2;
 };
 
 // Per-block ratio-test summary.
@@ -70,6 +73,8 @@ struct ERec {
     long long i;         // first column within the tie band of l
     double q;            // its value
     long long fneg;      // first column with c_j < -tol.cost
+    long long rule;      // k_group: block 0 publishes the rule for the next pivot here
+    long long pad[3];
 };
 
 // Deferred pivots: pivot s (0 <= s < ndef) of the current group is
@@ -101,6 +106,7 @@ struct Args {
     int nranks;
     int pad;
     lp_tol tol;
+    long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
 };
 
 // launch wrappers (kernels.hip).  t = index of the pivot within its group
@@ -115,6 +121,30 @@ hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max);  // nd_max >= ndef
+// one persistent launch selecting up to `count` chained pivots of a group
+hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec);
+constexpr int GROUP_BLOCKS = 64;   // co-resident workgroups of k_group (<= CUs) ...
+constexpr int GROUP_MAXBLOCKS = 256;
+constexpr int GROUP_ROWS = 64;     // ... raised so a block owns at most this many rows
+constexpr int GROUP_THREADS = 64;  // one wave: block reductions stay in registers
+constexpr long long GROUP_LDS_MAX = 96 * 1024;
+// dynamic LDS of one k_group block (own multipliers, pivot-row slices, row 0
+// and column 0 slices)
+__host__ __device__ inline long long group_lds(long long rc, long long ld, long long g, int count)
+{
+    const long long rpb = (rc + g - 1) / g, cpb = (ld + g - 1) / g;
+    return (rpb * count + count * cpb + cpb + rpb) * 8;
+}
+// workgroups of k_group for this shape, 0 if its LDS would not fit (the
+// per-pivot kernels are used instead)
+__host__ __device__ inline long long group_blocks(long long rc, long long ld, int count)
+{
+    long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
+    if (g < GROUP_BLOCKS) g = GROUP_BLOCKS;
+    while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count) > GROUP_LDS_MAX) g *= 2;
+    if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
+    return group_lds(rc, ld, g, count) > GROUP_LDS_MAX ? 0 : g;
+}
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
 __host__ __device__ inline int ratio_blocks(long long rows)
 {

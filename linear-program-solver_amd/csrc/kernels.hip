@@ -57,11 +57,13 @@ __device__ __forceinline__ long long wave_min_ll(long long v)
 }
 
 // block-wide minima; every thread gets the result.  scratch >= 16 entries.
+// A single-wave block reduces in registers only.
 __device__ double block_min(double v, double *scratch)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nw = (blockDim.x + 63) >> 6;
     v = wave_min(v);
+    if (nw == 1) return v;
     __syncthreads();
     if (lane == 0) scratch[wave] = v;
     __syncthreads();
@@ -75,6 +77,7 @@ __device__ long long block_min_ll(long long v, long long *scratch)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nw = (blockDim.x + 63) >> 6;
     v = wave_min_ll(v);
+    if (nw == 1) return v;
     __syncthreads();
     if (lane == 0) scratch[wave] = v;
     __syncthreads();
@@ -216,6 +219,9 @@ __global__ void k_reset(Args A, int mode, int rule, int chain, long long cap, lo
     ctl->ndef[1] = 0;
     ctl->z0 = -A.row0[0];
     ctl->ticket = 0;
+    ctl->bar[0] = 0;
+    ctl->bar[1] = 0;
+    ctl->bar_timeout = 0;
     A.dR[0] = r >= 0 ? local_of(A, r) : -1;
 }
 
@@ -270,35 +276,36 @@ __global__ void __launch_bounds__(ENTER_THREADS) k_enter(Args A)
     }
 }
 
-// entering column from k_prow's per-block row-0 summaries (block-wide, every
-// block gets the same answer): two-pass semantics of oracle/lp_f64.c's
-// entering().  The first summary block inside the global band holds the
-// answer -- its own candidate, or a rescan of its slice of row 0.
-__device__ long long combine_entering(const Args &A, int rule, double *sd, long long *sl)
+// entering column from per-block row-0 summaries (block-wide; every block
+// gets the same answer): two-pass semantics of oracle/lp_f64.c's entering().
+// Summary b covers row-0 columns [b*width, (b+1)*width).  The first summary
+// inside the global band holds the answer -- its own candidate, or a rescan
+// of its slice of row 0.  sc1 loads: valid right after a grid barrier too.
+__device__ long long combine_entering(const Args &A, int rule, unsigned nb, long long width,
+                                      double *sd, long long *sl)
 {
-    const unsigned nb = (unsigned)prow_blocks(A.ld);
     if (rule == LP_RULE_MIN_INDEX) {
         long long j = NONE;
         for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) {
-            const long long f = A.erec[b].fneg;
+            const long long f = ld_sc1(&A.erec[b].fneg);
             j = f < j ? f : j;
         }
         return block_min_ll(j, sl);
     }
     double g = INFINITY;
-    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) g = fmin(g, A.erec[b].l);
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) g = fmin(g, ld_sc1(&A.erec[b].l));
     g = block_min(g, sd);
     if (!(g < -A.tol.cost)) return NONE;
     const double thr = tie_band(g, A.tol.cost_tie);
     long long bsel = NONE;
     for (unsigned b = threadIdx.x; b < nb; b += blockDim.x)
-        if (A.erec[b].l <= thr) { bsel = b; break; }
+        if (ld_sc1(&A.erec[b].l) <= thr) { bsel = b; break; }
     bsel = block_min_ll(bsel, sl);
-    if (A.erec[bsel].q <= thr) return A.erec[bsel].i;
+    if (ld_sc1(&A.erec[bsel].q) <= thr) return ld_sc1(&A.erec[bsel].i);
     long long best = NONE;
-    const long long k0 = bsel * (long long)PROW_THREADS;
-    for (long long k = k0 + threadIdx.x; k < k0 + PROW_THREADS; k += blockDim.x)
-        if (k >= 1 && k <= A.n && A.row0[k] <= thr) { best = k; break; }
+    const long long k0 = bsel * width;
+    for (long long k = k0 + threadIdx.x; k < k0 + width; k += blockDim.x)
+        if (k >= 1 && k <= A.n && ld_sc1(&A.row0[k]) <= thr) { best = k; break; }
     return block_min_ll(best, sl);
 }
 
@@ -375,7 +382,7 @@ k_ratio(Args A, int t, int grp, int mode, int from_erec, long long check_row)
             if (mode == RATIO_LOCAL && blockIdx.x == 0 && threadIdx.x == 0) *A.xg = INFINITY;
             return;
         }
-        C = combine_entering(A, ctl->rule, sd, sl);
+        C = combine_entering(A, ctl->rule, (unsigned)prow_blocks(A.ld), PROW_THREADS, sd, sl);
         if (C == NONE) {
             if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_OPTIMAL;
             if (mode == RATIO_LOCAL && blockIdx.x == 0 && threadIdx.x == 0) *A.xg = INFINITY;
@@ -626,6 +633,388 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
 }
 
 // ---------------------------------------------------------------------------
+// K-group: every selection of one group of chained pivots in ONE persistent
+// launch (single device).  GROUP_BLOCKS co-resident workgroups; block b owns
+// a slice of the constraint rows (ratio test) and a slice of the columns
+// (pivot row, row 0).  Per pivot: entering column (combine of the row-0
+// summaries), ratio test on own rows -> summaries, grid barrier, leaving row
+// (combine of the ratio summaries), pivot row and row 0 on own columns ->
+// summaries, grid barrier.  Data shared across blocks inside the launch is
+// stored write-through (sc1) by drained waves and loaded sc1 after the
+// barrier's agent-scope counter (MI355X_MICROARCH "Valid forms" row 1).
+// Same float64 operations as k_ratio + k_prow; no host round trips.
+// ---------------------------------------------------------------------------
+
+// diagnostic: block 0 / lane 0 records the 100 MHz real-time clock at phase
+// points of pivot t (LPGPU_STAMPS=1 builds the buffer; nothing stored otherwise)
+__device__ __forceinline__ void stamp(const Args &A, int t, int k)
+{
+    if (A.stamps && blockIdx.x == 0 && threadIdx.x == 0 && t < BMAX)
+        A.stamps[t * 8 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
+// grid barrier k (1, 2, ...) of this launch: all blocks must be resident
+__device__ bool grid_barrier(unsigned *ctr, unsigned target, unsigned *timeout_flag, int *s_ok)
+{
+    drain_stores();   // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        int ok = 1;
+        while (ld_sc1(ctr) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 26)) {       // bounded: ~seconds, never expected
+                st_sc1(timeout_flag, 1u);
+                ok = 0;
+                break;
+            }
+        }
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// combine of G per-block summaries, loaded once into registers (summary
+// b = tid + k*blockDim, k < NR): two-pass semantics of the oracle.  Returns
+// the winning summary's candidate, or -1 - b when summary b is the first
+// inside the band but its own candidate is not (rare: rescan b's slice).
+constexpr int NR = (GROUP_MAXBLOCKS + GROUP_THREADS - 1) / GROUP_THREADS;
+
+__device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[NR],
+                                    const double (&q)[NR], unsigned G, double thr, long long *sl,
+                                    long long *s_sel)
+{
+    long long mine = NONE;       // first summary of this thread inside the band
+    int kmine = -1;
+#pragma unroll
+    for (int k = NR - 1; k >= 0; --k) {
+        const unsigned b = threadIdx.x + k * blockDim.x;
+        if (b < G && l[k] <= thr) { mine = b; kmine = k; }
+    }
+    const long long bsel = block_min_ll(mine, sl);
+    if (bsel == NONE) return NONE;
+    if (mine == bsel) {
+        s_sel[0] = q[kmine] <= thr ? i[kmine] : -1 - bsel;
+    }
+    __syncthreads();
+    return s_sel[0];
+}
+
+constexpr int IPL = 4;   // own rows / columns per lane kept in registers
+
+__global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int count, int from_erec)
+{
+    __shared__ double sd[16];
+    __shared__ long long sl[16];
+    __shared__ long long sR[BMAX];     // local pivot rows of this group
+    __shared__ double sPc[BMAX];       // P[s][C] for the current entering column
+    __shared__ double sMr[BMAX];       // M[R][s] for the current leaving row
+    __shared__ double s_q;
+    __shared__ int s_ok;
+    __shared__ long long s_sel[2];
+    // dynamic LDS: this block's rows' multipliers, its columns' pivot-row
+    // slices and its slices of row 0 / column 0 (own data never leaves LDS
+    // for a re-read; it is also published for the other blocks and the sweep)
+    extern __shared__ __attribute__((aligned(16))) double dyn[];
+    Ctl *ctl = A.ctl;
+    const unsigned G = gridDim.x, b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int nth = blockDim.x;
+    if (b == 0 && tid == 0) {          // the other parity's launch and sweep are complete
+        ctl->bar[grp ^ 1] = 0;
+        ctl->ndef[grp ^ 1] = 0;
+    }
+    if (ld_sc1(&ctl->status) != LP_PIVOTED) return;
+    unsigned *bar = &ctl->bar[grp];
+    unsigned nbar = 0;
+    const long long rpb = (A.rc + G - 1) / G;               // rows per block
+    const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
+    const long long cpb = (A.ld + G - 1) / G;               // columns per block
+    const long long jc0 = b * cpb, jc1 = min(jc0 + cpb, A.ld);
+    double *lM = dyn;                        // [rpb][count]
+    double *lP = lM + rpb * count;           // [count][cpb]
+    double *l0 = lP + count * cpb;           // [cpb]  row 0 slice
+    double *lc = l0 + cpb;                   // [rpb]  column 0 slice
+    for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = A.row0[j];
+    for (long long li = lr0 + tid; li < lr1; li += nth) lc[li - lr0] = A.col0[li];
+    const long long cap = ctl->cap;
+    const int mode = ctl->mode;
+    // counters live in registers for the launch (block 0 publishes them)
+    long long npiv = ld_sc1(&ctl->npiv);
+    int rule = ld_sc1(&ctl->rule);
+    long long nstd = 0, stuck = 0;
+    double z0 = 0.0;
+    if (b == 0 && tid == 0) {
+        nstd = ctl->nstd;
+        stuck = ctl->stuck;
+        z0 = ctl->z0;
+    }
+    int status = LP_PIVOTED;
+    int pending = -1;                 // pivot whose column-0 update is still due
+    long long pendR = -1;
+    __syncthreads();
+    for (int t = 0; t < count; ++t) {
+        stamp(A, t, 0);
+        // ---- entering column (+ the previous pivot's column-0 update, whose
+        //      P[.][0] load shares the round trip with the summaries)
+        long long C;
+        double p0 = 0.0;
+        if (pending >= 0) p0 = ld_sc1(&A.P[pending * A.ld]);
+        if (t == 0 && !from_erec) {
+            C = ld_sc1(&ctl->c) + 1;
+        } else {
+            const bool capped = cap >= 0 && npiv >= cap;
+            double el[NR], eq[NR];
+            long long ei[NR];
+            long long ef = NONE;
+            double emin = INFINITY;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const unsigned bb = tid + k * nth;
+                el[k] = INFINITY;
+                eq[k] = 0.0;
+                ei[k] = NONE;
+                if (bb < G) {
+                    el[k] = ld_sc1(&A.erec[bb].l);
+                    ei[k] = ld_sc1(&A.erec[bb].i);
+                    eq[k] = ld_sc1(&A.erec[bb].q);
+                    const long long f = ld_sc1(&A.erec[bb].fneg);
+                    ef = f < ef ? f : ef;
+                    emin = fmin(emin, el[k]);
+                }
+            }
+            // the rule (stall switch) arrives in block 0's summary, same round trip
+            long long rr = tid == 0 ? ld_sc1(&A.erec[0].rule) : 0;
+            rule = (int)__shfl(rr, 0, 64);
+            if (capped) {
+                C = NONE;
+            } else if (rule == LP_RULE_MIN_INDEX) {
+                C = block_min_ll(ef, sl);
+            } else {
+                const double g = block_min(emin, sd);
+                if (!(g < -A.tol.cost)) {
+                    C = NONE;
+                } else {
+                    const double ethr = tie_band(g, A.tol.cost_tie);
+                    C = combine_loaded(el, ei, eq, G, ethr, sl, s_sel);
+                    if (C < 0) {   // rare: rescan that slice of row 0
+                        const long long k0 = (-1 - C) * cpb;
+                        long long best = NONE;
+                        for (long long k = k0 + tid; k < k0 + cpb; k += nth)
+                            if (k >= 1 && k <= A.n && ld_sc1(&A.row0[k]) <= ethr) { best = k; break; }
+                        C = block_min_ll(best, sl);
+                    }
+                }
+            }
+            if (C == NONE) status = capped ? LP_CAP_REACHED : LP_OPTIMAL;
+        }
+        if (pending >= 0) {
+            for (long long li = lr0 + tid; li < lr1; li += nth) {
+                const long long k = li - lr0;
+                const double c0 = upd(li, pendR, lM[k * count + pending], p0, lc[k]);
+                lc[k] = c0;
+                st_sc1(&A.col0[li], c0);
+            }
+            pending = -1;
+        }
+        if (status != LP_PIVOTED) break;
+        stamp(A, t, 1);
+        // ---- ratio test over own rows; M[t] of own rows.  The tableau column
+        //      loads are issued before the cross-block loads (one round trip).
+        double av[IPL];
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const long long li = lr0 + tid + k * nth;
+            av[k] = li < lr1 ? A.T[li * A.ld + C] : 0.0;
+        }
+        if (tid < t) sPc[tid] = ld_sc1(&A.P[tid * A.ld + C]);
+        if (tid == 0) {
+            if (b == 0) st_sc1(&ctl->c, C - 1);
+            if (C >= jc0 && C < jc1) st_sc1(&A.M[t], l0[C - jc0]);   // row 0's multiplier
+        }
+        __syncthreads();
+        double lbest = INFINITY;
+        auto ratio_row = [&](long long li, double a) {
+            const long long k = li - lr0;
+            for (int s2 = 0; s2 < t; ++s2) a = upd(li, sR[s2], lM[k * count + s2], sPc[s2], a);
+            lM[k * count + t] = a;
+            st_sc1(&A.M[li * BMAX + t], a);
+            bool ok;
+            const double q = row_ratio(a, lc[k], A.tol, ok);
+            if (ok) lbest = fmin(lbest, q);
+        };
+#pragma unroll
+        for (int k2 = 0; k2 < IPL; ++k2) {
+            const long long li = lr0 + tid + k2 * nth;
+            if (li < lr1) ratio_row(li, av[k2]);
+        }
+        for (long long li = lr0 + tid + IPL * nth; li < lr1; li += nth)
+            ratio_row(li, A.T[li * A.ld + C]);
+        const double lb = block_min(lbest, sd);
+        long long ib = NONE;
+        double qb = 0.0;
+        if (lb < INFINITY) {
+            const double thr = tie_band(lb, A.tol.ratio_tie);
+            long long mine = NONE;
+            double qmine = 0.0;
+            for (long long li = lr0 + tid; li < lr1; li += nth) {
+                bool ok;
+                const double q = row_ratio(lM[(li - lr0) * count + t], lc[li - lr0], A.tol, ok);
+                if (ok && q <= thr) { mine = li; qmine = q; break; }
+            }
+            ib = block_min_ll(mine, sl);
+            if (mine == ib) s_q = qmine;
+            __syncthreads();
+            qb = s_q;
+        }
+        if (tid == 0) {
+            st_sc1(&A.rec[b].l, lb);
+            st_sc1(&A.rec[b].i, ib);
+            st_sc1(&A.rec[b].q, qb);
+        }
+        stamp(A, t, 2);
+        if (!grid_barrier(bar, G * ++nbar, &ctl->bar_timeout, &s_ok)) { status = LP_DEVICE_ERROR; break; }
+        stamp(A, t, 3);
+
+        // ---- leaving row (combine the ratio summaries: one load each)
+        double rl[NR], rq[NR];
+        long long ri[NR];
+        double rmin = INFINITY;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const unsigned bb = tid + k * nth;
+            rl[k] = INFINITY;
+            rq[k] = 0.0;
+            ri[k] = NONE;
+            if (bb < G) {
+                rl[k] = ld_sc1(&A.rec[bb].l);
+                ri[k] = ld_sc1(&A.rec[bb].i);
+                rq[k] = ld_sc1(&A.rec[bb].q);
+                rmin = fmin(rmin, rl[k]);
+            }
+        }
+        const double g = block_min(rmin, sd);
+        if (!(g < INFINITY)) { status = LP_UNBOUNDED; break; }
+        const double thr = tie_band(g, A.tol.ratio_tie);
+        long long R = combine_loaded(rl, ri, rq, G, thr, sl, s_sel);
+        if (R < 0) {   // rare: rescan the selected block's rows (their M[t], col0 are published)
+            const long long bsel = -1 - R;
+            const long long r0 = 1 + bsel * rpb, r1 = min(r0 + rpb, A.rows);
+            long long mine = NONE;
+            for (long long li = r0 + tid; li < r1; li += nth) {
+                bool ok;
+                const double q = row_ratio(ld_sc1(&A.M[li * BMAX + t]), ld_sc1(&A.col0[li]), A.tol, ok);
+                if (ok && q <= thr) { mine = li; break; }
+            }
+            R = block_min_ll(mine, sl);
+        }
+        stamp(A, t, 4);
+        // ---- pivot row on own columns, row 0 on own columns.  Tableau row
+        //      loads first, then the cross-block loads (one round trip).
+        double xv[IPL];
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const long long j = jc0 + tid + k * nth;
+            xv[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
+        }
+        if (tid <= t) sMr[tid] = ld_sc1(&A.M[R * BMAX + tid]);
+        if (tid == 0) sR[t] = R;
+        const double f0 = ld_sc1(&A.M[t]);
+        __syncthreads();
+        const double a = sMr[t];
+        double vmin = INFINITY, v0 = 0.0;
+        long long fneg = NONE;
+        auto prow_col = [&](long long j, double x) {
+            const long long k = j - jc0;
+            for (int s2 = 0; s2 < t; ++s2) x = upd(R, sR[s2], sMr[s2], lP[s2 * cpb + k], x);
+            const double p = (j == C) ? 1.0 : x / a;
+            lP[t * cpb + k] = p;
+            st_sc1(&A.P[t * A.ld + j], p);
+            const double v = upd(0, -1, f0, p, l0[k]);
+            l0[k] = v;
+            st_sc1(&A.row0[j], v);
+            if (j == 0) v0 = v;
+            if (j >= 1 && j <= A.n) {
+                vmin = fmin(vmin, v);
+                if (v < -A.tol.cost && j < fneg) fneg = j;
+            }
+        };
+#pragma unroll
+        for (int k2 = 0; k2 < IPL; ++k2) {
+            const long long j = jc0 + tid + k2 * nth;
+            if (j < jc1) prow_col(j, xv[k2]);
+        }
+        for (long long j = jc0 + tid + IPL * nth; j < jc1; j += nth) prow_col(j, A.T[R * A.ld + j]);
+        // row-0 summary of own columns
+        const double el = block_min(vmin, sd);
+        const long long efn = block_min_ll(fneg, sl);
+        long long ei = NONE;
+        double eq = 0.0;
+        if (el < INFINITY) {
+            const double ethr = tie_band(el, A.tol.cost_tie);
+            long long mine = NONE;
+            double vmine = 0.0;
+            for (long long j = jc0 + tid; j < jc1; j += nth) {
+                const double v = l0[j - jc0];
+                if (j >= 1 && j <= A.n && v <= ethr) { mine = j; vmine = v; break; }
+            }
+            ei = block_min_ll(mine, sl);
+            if (mine == ei) s_q = vmine;
+            __syncthreads();
+            eq = s_q;
+        }
+        if (b == 0 && tid == 0) {     // column 0 is in block 0's slice: v0 = new row0[0]
+            const long long rglob = R - 1 + A.rb;
+            st_sc1(&A.dR[t], R);
+            st_sc1(&A.dC[t], C);
+            st_sc1(&ctl->r, rglob);
+            if (npiv < A.logcap) {
+                A.log[2 * npiv] = rglob;
+                A.log[2 * npiv + 1] = C - 1;
+            }
+            st_sc1(&ctl->npiv, npiv + 1);
+            st_sc1(&ctl->ndef[grp], (long long)(t + 1));
+            if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
+                nstd += 1;
+                // stall bookkeeping (simplex.py:132-137), min-index switch (:123,138)
+                const double z = -v0;
+                if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) stuck += 1;
+                else stuck = 0;
+                if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
+                st_sc1(&ctl->nstd, nstd);
+                st_sc1(&ctl->stuck, stuck);
+                st_sc1(&ctl->rule, rule);
+            }
+            st_sc1(&A.erec[0].rule, (long long)rule);
+        }
+        if (tid == 0) {
+            st_sc1(&A.erec[b].l, el);
+            st_sc1(&A.erec[b].i, ei);
+            st_sc1(&A.erec[b].q, eq);
+            st_sc1(&A.erec[b].fneg, efn);
+        }
+        ++npiv;
+        stamp(A, t, 5);
+        if (!grid_barrier(bar, G * ++nbar, &ctl->bar_timeout, &s_ok)) { status = LP_DEVICE_ERROR; break; }
+        stamp(A, t, 6);
+        pending = t;
+        pendR = R;
+        stamp(A, t, 7);
+    }
+    // the last pivot's column-0 update (P[.][0] is published: barrier passed)
+    if (pending >= 0) {
+        const double p0 = ld_sc1(&A.P[pending * A.ld]);
+        for (long long li = lr0 + tid; li < lr1; li += nth) {
+            const long long k = li - lr0;
+            st_sc1(&A.col0[li], upd(li, pendR, lM[k * count + pending], p0, lc[k]));
+        }
+    }
+    if (b == 0 && tid == 0 && status != LP_PIVOTED) st_sc1(&ctl->status, status);
+}
+
+// ---------------------------------------------------------------------------
 // K3: the sweep.  T <- T with the group's deferred pivots 0..ndef-1 applied.
 //   Tile = 128 columns (one wave: 64 lanes x 16 B) x SWEEP_ROWS rows; the
 //   four waves of a block take interleaved rows.  Each lane keeps its slice
@@ -810,6 +1199,17 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max)
         SWEEP_CASE(32)
     }
 #undef SWEEP_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec)
+{
+    if (count < 1 || count > BMAX) return hipErrorInvalidValue;
+    const long long g = group_blocks(A.rc, A.ld, count);
+    if (g == 0) return hipErrorInvalidValue;
+    const size_t lds = (size_t)group_lds(A.rc, A.ld, g, count);
+    hipLaunchKernelGGL(k_group, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp, count,
+                       from_erec);
     return hipGetLastError();
 }
 

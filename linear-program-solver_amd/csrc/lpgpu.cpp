@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -40,7 +41,9 @@ struct lp_handle {
     double *T = nullptr, *P = nullptr, *M = nullptr, *row0 = nullptr, *col0 = nullptr;
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
-    int block = 8;                  // pivots deferred into one sweep (1..BMAX)
+    int block = 16;                 // pivots deferred into one sweep (1..BMAX)
+    bool persistent = true;         // single device: one k_group launch per group
+    long long *stamps = nullptr;    // diagnostic phase clocks (LPGPU_STAMPS=1)
     bool eager_ok = false;          // row0/col0 mirror the stored tableau
     Ctl *ctl = nullptr;
     Ctl *hctl = nullptr;            // pinned mirror
@@ -188,6 +191,7 @@ static Args args_of(const lp_handle *h)
     A.nranks = h->nranks;
     A.pad = 0;
     A.tol = h->tol;
+    A.stamps = h->stamps;
     return A;
 }
 
@@ -223,6 +227,13 @@ static void init_geometry(lp_handle *h, int64_t m, int64_t n, int rank, int nran
 
 static int alloc_handle(lp_handle *h)
 {
+    if (const char *sel = std::getenv("LPGPU_SELECT"))
+        h->persistent = std::strcmp(sel, "kernels") != 0;
+    if (const char *st = std::getenv("LPGPU_STAMPS"))
+        if (st[0] == '1') {
+            HCHK(h, hipMalloc(&h->stamps, lpk::BMAX * 8 * sizeof(long long)));
+            HCHK(h, hipMemset(h->stamps, 0, lpk::BMAX * 8 * sizeof(long long)));
+        }
     HCHK(h, hipSetDevice(h->dev));
     if (!h->s) HCHK(h, hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
     const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
@@ -238,7 +249,8 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMemsetAsync(h->col0, 0, (size_t)h->rows * sizeof(double), h->s));
     HCHK(h, hipMalloc(&h->dR, (size_t)lpk::BMAX * sizeof(long long)));
     HCHK(h, hipMalloc(&h->dC, (size_t)lpk::BMAX * sizeof(long long)));
-    HCHK(h, hipMalloc(&h->erec, (size_t)std::max(1, lpk::prow_blocks(h->ld)) * sizeof(lpk::ERec)));
+    HCHK(h, hipMalloc(&h->erec, (size_t)std::max(lpk::GROUP_MAXBLOCKS, lpk::prow_blocks(h->ld)) *
+                                     sizeof(lpk::ERec)));
     h->eager_ok = true;   // all zero
     HCHK(h, hipMalloc(&h->ctl, sizeof(Ctl)));
     HCHK(h, hipMemsetAsync(h->ctl, 0, sizeof(Ctl), h->s));
@@ -246,7 +258,7 @@ static int alloc_handle(lp_handle *h)
     std::memset(h->hctl, 0, sizeof(Ctl));
     h->logcap = 4096;
     HCHK(h, hipMalloc(&h->log, (size_t)h->logcap * 2 * sizeof(long long)));
-    const int nrec = std::max(1, lpk::ratio_blocks(h->rows));
+    const int nrec = std::max(lpk::GROUP_MAXBLOCKS, lpk::ratio_blocks(h->rows));
     HCHK(h, hipMalloc(&h->rec, (size_t)nrec * sizeof(Rec)));
     HCHK(h, hipMemsetAsync(h->rec, 0, (size_t)nrec * sizeof(Rec), h->s));
     if (h->nranks > 1 || h->comm) {
@@ -395,6 +407,7 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->dR) (void)hipFree(h->dR);
     if (h->dC) (void)hipFree(h->dC);
     if (h->erec) (void)hipFree(h->erec);
+    if (h->stamps) (void)hipFree(h->stamps);
     if (h->ctl) (void)hipFree(h->ctl);
     if (h->hctl) (void)hipHostFree(h->hctl);
     if (h->log) (void)hipFree(h->log);
@@ -654,17 +667,28 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         if (limit >= 0) b = std::min(b, limit - enq);
         for (lp_handle *x : M) CALL(ensure_log(x, enq + b));
         A = args_all(M);
-        int t = 0;
-        for (int64_t k = 0; k < b; ++k) {
-            CALL(enqueue_select(M, A, t, grp, 0, enq + k > 0 ? 1 : 0, false));
-            if (++t == B || k + 1 == b) {
+        if (!h->comm && h->persistent && lpk::group_blocks(h->rc, h->ld, B) > 0) {
+            // one persistent selection launch + one sweep per group
+            for (int64_t k = 0; k < b; k += B) {
+                const int cnt = (int)std::min<int64_t>(B, b - k);
+                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, enq + k > 0 ? 1 : 0));
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
-                t = 0;
+            }
+        } else {
+            int t = 0;
+            for (int64_t k = 0; k < b; ++k) {
+                CALL(enqueue_select(M, A, t, grp, 0, enq + k > 0 ? 1 : 0, false));
+                if (++t == B || k + 1 == b) {
+                    CALL(enqueue_sweep(M, A, grp));
+                    grp ^= 1;
+                    t = 0;
+                }
             }
         }
         enq += b;
         CALL(sync_ctl(M));
+        if (h->hctl->bar_timeout) return fail(h, LP_DEVICE_ERROR, "k_group grid barrier timed out");
         if (h->hctl->status != LP_PIVOTED) return h->hctl->status;
         if (limit >= 0 && enq >= limit) return LP_PIVOTED;
         batch = std::min<int64_t>(batch * 2, std::max<int64_t>(1024, 32 * B));
@@ -770,5 +794,13 @@ extern "C" int lp_update_time(lp_handle *h, double *ms, int64_t *launches)
 {
     *ms = h->prof_ms;
     *launches = h->prof_n;
+    return LP_PIVOTED;
+}
+
+// diagnostic (not part of the C-ABI): k_group phase clocks of the last group
+extern "C" int lpdiag_stamps(lp_handle *h, long long *out)
+{
+    if (!h->stamps) return LP_BAD_ARG;
+    HCHK(h, hipMemcpy(out, h->stamps, lpk::BMAX * 8 * sizeof(long long), hipMemcpyDeviceToHost));
     return LP_PIVOTED;
 }

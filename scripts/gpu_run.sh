@@ -25,6 +25,13 @@ for step in "$@"; do
             for B in 1 2 4 8 16 32; do
                 run bench_b$B 300 python bench.py --no-cpu-baseline --block $B
             done ;;
+        psweep)
+            for B in 4 8 16 32; do
+                run benchp_b$B 300 python bench.py --no-cpu-baseline --block $B
+            done
+            LPGPU_SELECT=kernels run benchk_b16 300 python bench.py --no-cpu-baseline --block 16 ;;
+        cfg4one)
+            run bench_cfg4_1gpu 600 python bench.py --no-cpu-baseline --block 16 --emulate-ranks 8 --steps 256 ;;
         prof16)
             export TMPDIR=/tmp
             run rocprof16 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof16" -o run -- python3 "$PWD/bench.py" --steps 512 --block 16 --no-cpu-baseline ;;

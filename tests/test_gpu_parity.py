@@ -45,6 +45,14 @@ def _initial_basis(T):
     return bc
 
 
+@pytest.fixture(params=["persistent", "kernels"])
+def select_mode(request, monkeypatch):
+    """single-device selection path: one persistent k_group launch per group,
+    or the per-pivot k_ratio/k_prow launches (the sharded path's kernels)"""
+    monkeypatch.setenv("LPGPU_SELECT", request.param)
+    return request.param
+
+
 def engine_of(T, block=8):
     e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
     e.upload(T)
@@ -77,7 +85,7 @@ def test_reference_kat_pivot_pair():
 # ----------------------------------------------------------- golden solves
 @pytest.mark.parametrize("block", [1, 8])
 @pytest.mark.parametrize("fx", SMALL["solve"] + BIG["solve"], ids=_ids(SMALL["solve"] + BIG["solve"]))
-def test_solve_matches_reference(fx, block):
+def test_solve_matches_reference(fx, block, select_mode):
     T = fixture_input(fx)
     e = engine_of(T, block)
     st, npiv, nstd = e.solve()
@@ -93,7 +101,7 @@ def test_solve_matches_reference(fx, block):
 @pytest.mark.parametrize("fx", SMALL["standard_k"] + BIG["standard_k"],
                          ids=_ids(SMALL["standard_k"] + BIG["standard_k"]))
 @pytest.mark.parametrize("block", [1, 5, 32])
-def test_standard_k_matches_reference(fx, block):
+def test_standard_k_matches_reference(fx, block, select_mode):
     T = fixture_input(fx)
     e = engine_of(T, block)
     st, done = e.run(_lib.RULE_STANDARD, fx["k"])
@@ -189,7 +197,7 @@ def test_optimal_at_start_and_cap():
     ("tall", 1000, 2, 10), ("tall", 2, 5000, 10), ("mixed", 255, 129, 40),
 ])
 @pytest.mark.parametrize("block", [1, 7, 32])
-def test_ragged_shapes_bit_exact(kind, m, ns, k, block):
+def test_ragged_shapes_bit_exact(kind, m, ns, k, block, select_mode):
     T = gen.tableau(kind, m, ns, 77)
     e = engine_of(T, block)
     st, done = e.run(_lib.RULE_STANDARD, k)
@@ -200,7 +208,7 @@ def test_ragged_shapes_bit_exact(kind, m, ns, k, block):
 
 
 @pytest.mark.parametrize("block", [1, 32])
-def test_cfg3_full_size_bit_exact(block):
+def test_cfg3_full_size_bit_exact(block, select_mode):
     """4096 x 8192 (the 1-GPU roofline config): 40 standard pivots, whole
     268 MB tableau bit-identical to the f64 oracle."""
     T = gen.tableau("mixed", 4096, 4096, 3)
@@ -290,7 +298,7 @@ def test_sweep_kernel_event_timing():
     assert n == 3 and ms > 0
 
 
-def test_block_size_invariance():
+def test_block_size_invariance(select_mode):
     """every deferral depth gives the same bits (the sweep replays the exact
     per-pivot float64 operations)"""
     T = gen.tableau("mixed", 200, 300, 5)
