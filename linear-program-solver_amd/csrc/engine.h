@@ -20,12 +20,19 @@ constexpr int RATIO_CHECK = 2;  // validate a given row (Simplex.pivot)
 // where k_prow finds the leaving row
 constexpr int RSRC_RECORDS = 0;  // combine k_ratio's per-block records
 constexpr int RSRC_GIVEN = 1;    // dR[t] set by the caller (Tableau.pivot / Simplex.pivot)
-constexpr int RSRC_SLOTS = 2;    // sharded: the gathered rank slots
+constexpr int RSRC_SLOTS = 2;    // sharded: lowest row index offered in the gathered slots
+constexpr int RSRC_BAND = 3;     // sharded, one exchange: band test on the slots' (l, q)
+
+// internal status (never returned through the C-ABI): the one-exchange
+// protocol met a near-tie straddling the tie band; the host redoes that
+// pivot with the two-exchange protocol (oracle/sharded_model.py step 4)
+constexpr int ST_STRADDLE = 3;
 
 // k_pick modes (sharded)
 constexpr int PICK_RATIO = 0;     // first local row within the tie band of the global min
 constexpr int PICK_CHECK = 1;     // owner validates the requested row (Simplex.pivot)
 constexpr int PICK_EXPLICIT = 2;  // owner contributes the requested row (Tableau.pivot)
+constexpr int PICK_LOCAL = 3;     // first local row within the LOCAL band + (l, q)
 
 constexpr int BMAX = 32;           // most pivots deferred into one sweep
 constexpr int RATIO_THREADS = 256;
@@ -146,6 +153,7 @@ __host__ __device__ inline long long group_blocks(long long rc, long long ld, in
     return group_lds(rc, ld, g, count) > GROUP_LDS_MAX ? 0 : g;
 }
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
+hipError_t launch_resume(hipStream_t s, const Args &A);
 __host__ __device__ inline int ratio_blocks(long long rows)
 {
     return (int)((rows - 1 + RATIO_CHUNK - 1) / RATIO_CHUNK);

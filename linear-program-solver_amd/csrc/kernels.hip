@@ -466,7 +466,19 @@ __global__ void __launch_bounds__(256) k_pick(Args A, int t, int mode)
     const long long C = ctl->c + 1;
     long long li = -1;
     long long code = 0;
-    if (mode == PICK_RATIO) {
+    double lloc = INFINITY, qloc = 0.0;
+    if (mode == PICK_LOCAL) {
+        // one-exchange protocol: this rank's minimum and first in-band row
+        __shared__ double sd[16];
+        lloc = records_min(A, sd);
+        if (lloc < INFINITY) {
+            const long long w = pick_from_records(A, t, C, lloc, sl);
+            li = w;
+            bool ok;
+            const double a = current(A, t, w, C, A.T[w * A.ld + C]);
+            qloc = row_ratio(a, A.col0[w], A.tol, ok);
+        }
+    } else if (mode == PICK_RATIO) {
         const double g = *A.xg;
         if (!(g < INFINITY)) {
             // every rank holds the same global minimum: unbounded everywhere
@@ -490,6 +502,8 @@ __global__ void __launch_bounds__(256) k_pick(Args A, int t, int mode)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.xs[0] = as_d(li < 0 ? NONE : li - 1 + A.rb);
         A.xs[1] = as_d(code);
+        A.xs[2] = lloc;
+        A.xs[3] = qloc;
     }
     if (li < 0) return;
     for (long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x; j < A.ld;
@@ -527,15 +541,36 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
     long long R, rglob;
     double a;
     const double *src = nullptr;   // sharded: the current pivot row from its owner
-    if (rsrc == RSRC_SLOTS) {
+    if (rsrc == RSRC_SLOTS || rsrc == RSRC_BAND) {
         const long long slot = SLOT_HDR + A.ld;
         long long best = NONE, code = 0;
         int who = -1;
-        for (int k = 0; k < A.nranks; ++k) {
-            const long long idx = as_ll(A.xr[k * slot]);
-            const long long cd = as_ll(A.xr[k * slot + 1]);
-            if (cd != 0) code = cd;
-            if (idx < best) { best = idx; who = k; }
+        if (rsrc == RSRC_BAND) {
+            // ranks hold consecutive row blocks: the first rank whose minimum
+            // is inside the global band holds the first in-band row, provided
+            // its own first in-band row is inside the global band too
+            double g = INFINITY;
+            for (int k = 0; k < A.nranks; ++k) g = fmin(g, A.xr[k * slot + 2]);
+            if (!(g < INFINITY)) {
+                if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_UNBOUNDED;
+                return;
+            }
+            const double thr = tie_band(g, A.tol.ratio_tie);
+            int k = 0;
+            while (!(A.xr[k * slot + 2] <= thr)) ++k;
+            if (!(A.xr[k * slot + 3] <= thr)) {
+                if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = ST_STRADDLE;
+                return;
+            }
+            best = as_ll(A.xr[k * slot]);
+            who = k;
+        } else {
+            for (int k = 0; k < A.nranks; ++k) {
+                const long long idx = as_ll(A.xr[k * slot]);
+                const long long cd = as_ll(A.xr[k * slot + 1]);
+                if (cd != 0) code = cd;
+                if (idx < best) { best = idx; who = k; }
+            }
         }
         if (code != 0 || best == NONE) {
             if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -1097,6 +1132,14 @@ k_sweep(double *__restrict__ T, const double *__restrict__ P, const double *__re
     }
 }
 
+// after a straddle: the group was swept up to the straddling pivot; continue
+__global__ void k_resume(Ctl *ctl)
+{
+    ctl->status = LP_PIVOTED;
+    ctl->ndef[0] = 0;
+    ctl->ndef[1] = 0;
+}
+
 // in-process shard group: allreduce-min of one double across n device buffers
 __global__ void k_group_min(double *const *ptrs, int n)
 {
@@ -1210,6 +1253,12 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
     const size_t lds = (size_t)group_lds(A.rc, A.ld, g, count);
     hipLaunchKernelGGL(k_group, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp, count,
                        from_erec);
+    return hipGetLastError();
+}
+
+hipError_t launch_resume(hipStream_t s, const Args &A)
+{
+    hipLaunchKernelGGL(k_resume, dim3(1), dim3(1), 0, s, A.ctl);
     return hipGetLastError();
 }
 

@@ -593,7 +593,7 @@ static std::vector<Args> args_all(const Members &M)
 // pivot's row-0 summaries (chained pivots).  peek: stop once the leaving row
 // is known (findPivot*(False)).
 static int enqueue_select(const Members &M, const std::vector<Args> &A, int t, int grp, int sel,
-                          int from_erec, bool peek)
+                          int from_erec, bool peek, bool one_exchange = false)
 {
     lp_handle *h0 = M[0];
     if (!h0->comm) {
@@ -607,6 +607,18 @@ static int enqueue_select(const Members &M, const std::vector<Args> &A, int t, i
             else HCHK(h0, lpk::launch_gather(h0->s, A[0], t));
             HCHK(h0, lpk::launch_prow(h0->s, A[0], t, grp, lpk::RSRC_GIVEN, 0));
         }
+        return LP_PIVOTED;
+    }
+    if (sel == 0 && one_exchange && !peek) {
+        // one allgather per pivot: (index, local min, ratio, current row) per
+        // rank; a near-tie straddling the band stops with ST_STRADDLE
+        for (size_t k = 0; k < M.size(); ++k)
+            HCHK(M[k], lpk::launch_ratio(M[k]->s, A[k], t, grp, lpk::RATIO_FULL, from_erec, -1));
+        for (size_t k = 0; k < M.size(); ++k)
+            HCHK(M[k], lpk::launch_pick(M[k]->s, A[k], t, lpk::PICK_LOCAL));
+        CALL(h0->comm->allgather(M));
+        for (size_t k = 0; k < M.size(); ++k)
+            HCHK(M[k], lpk::launch_prow(M[k]->s, A[k], t, grp, lpk::RSRC_BAND, 0));
         return LP_PIVOTED;
     }
     for (size_t k = 0; k < M.size(); ++k) {
@@ -659,26 +671,29 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
     CALL(begin_call(M, A, mode, rule, 1, cap, -1, -1));
     for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
     const int B = h->block;
-    int64_t enq = 0;
+    int64_t done = 0;      // pivots performed (device count)
     int64_t batch = 8 * B;
     int grp = 0;
+    bool chained = false;  // the next pivot's entering column comes from k_prow
     for (;;) {
         int64_t b = batch;
-        if (limit >= 0) b = std::min(b, limit - enq);
-        for (lp_handle *x : M) CALL(ensure_log(x, enq + b));
+        if (limit >= 0) b = std::min(b, limit - done);
+        for (lp_handle *x : M) CALL(ensure_log(x, done + b + 1));
         A = args_all(M);
         if (!h->comm && h->persistent && lpk::group_blocks(h->rc, h->ld, B) > 0) {
             // one persistent selection launch + one sweep per group
             for (int64_t k = 0; k < b; k += B) {
                 const int cnt = (int)std::min<int64_t>(B, b - k);
-                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, enq + k > 0 ? 1 : 0));
+                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0));
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
+                chained = true;
             }
         } else {
             int t = 0;
             for (int64_t k = 0; k < b; ++k) {
-                CALL(enqueue_select(M, A, t, grp, 0, enq + k > 0 ? 1 : 0, false));
+                CALL(enqueue_select(M, A, t, grp, 0, chained ? 1 : 0, false, true));
+                chained = true;
                 if (++t == B || k + 1 == b) {
                     CALL(enqueue_sweep(M, A, grp));
                     grp ^= 1;
@@ -686,11 +701,20 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
                 }
             }
         }
-        enq += b;
         CALL(sync_ctl(M));
         if (h->hctl->bar_timeout) return fail(h, LP_DEVICE_ERROR, "k_group grid barrier timed out");
+        if (h->hctl->status == lpk::ST_STRADDLE) {
+            // rare near-tie across ranks: the pivots before it are swept and
+            // ctl->c holds its entering column; redo it with two exchanges
+            for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_resume(M[k]->s, A[k]));
+            CALL(enqueue_select(M, A, 0, grp, 0, 0, false, false));
+            CALL(enqueue_sweep(M, A, grp));
+            grp ^= 1;
+            CALL(sync_ctl(M));
+        }
+        done = h->hctl->npiv;
         if (h->hctl->status != LP_PIVOTED) return h->hctl->status;
-        if (limit >= 0 && enq >= limit) return LP_PIVOTED;
+        if (limit >= 0 && done >= limit) return LP_PIVOTED;
         batch = std::min<int64_t>(batch * 2, std::max<int64_t>(1024, 32 * B));
     }
 }

@@ -160,3 +160,59 @@ int lpf_solve(double *T, int64_t m, int64_t n, int64_t ld, const lp_tol *tol,
         }
     }
 }
+
+/* ---- pieces of one pivot, for the row-sharded protocol model ------------- */
+
+/* P = row / row[C], P[C] = 1  (the normalised pivot row) */
+void lpf_prow(const double *row, int64_t n, int64_t C, double *P)
+{
+    const double a = row[C];
+    for (int64_t j = 0; j <= n; ++j) P[j] = row[j] / a;
+    P[C] = 1.0;
+}
+
+/* apply the pivot (P, tableau column C) to `rows` stored rows; local row
+ * Rloc (or -1) becomes P, every other row gets fma(-f, P[j], x) */
+void lpf_apply(double *T, int64_t rows, int64_t n, int64_t ld, const double *P, int64_t C,
+               int64_t Rloc)
+{
+    for (int64_t i = 0; i < rows; ++i) {
+        double *t = T + i * ld;
+        if (i == Rloc) {
+            for (int64_t j = 0; j <= n; ++j) t[j] = P[j];
+            continue;
+        }
+        const double f = t[C];
+        for (int64_t j = 0; j <= n; ++j) t[j] = fma(-f, P[j], t[j]);
+    }
+}
+
+/* ratio-test pieces over `rows` stored constraint rows (no row 0):
+ * *lmin = min ratio (INFINITY if none eligible); returns the first row with
+ * ratio <= thr (or -1) and its ratio in *q */
+double lpf_min_ratio(const double *T, int64_t rows, int64_t ld, int64_t C, const lp_tol *tol)
+{
+    double g = INFINITY;
+    for (int64_t i = 0; i < rows; ++i) {
+        int ok;
+        const double q = ratio_of(T + i * ld, C, tol, &ok);
+        if (ok && q < g) g = q;
+    }
+    return g;
+}
+
+int64_t lpf_first_within(const double *T, int64_t rows, int64_t ld, int64_t C, const lp_tol *tol,
+                         double thr, double *q_out)
+{
+    for (int64_t i = 0; i < rows; ++i) {
+        int ok;
+        const double q = ratio_of(T + i * ld, C, tol, &ok);
+        if (ok && q <= thr) { *q_out = q; return i; }
+    }
+    return -1;
+}
+
+int64_t lpf_entering(const double *row0, int64_t n, int rule, const lp_tol *tol)
+{
+    return entering(row0, n, rule, tol);
+}

@@ -327,3 +327,38 @@ def test_find_without_pivot_leaves_tableau_untouched():
             assert np.array_equal(g.rows(1 + b, c), o.T[1 + b:1 + b + c])
         for g in reversed(grp):
             g.close()
+
+
+def _straddle_tableau():
+    T = np.zeros((5, 6))
+    T[0, 1] = -1.0
+    T[1:, 0] = [1.2, 1.0, 0.9, 2.0]
+    T[1:, 1] = 1.0
+    T[1:, 2:] = np.eye(4)
+    return T
+
+
+@pytest.mark.parametrize("kind,tie,nshards,k", [
+    ("straddle", 0.25, 2, 1), ("mixed", 0.25, 3, 40), ("mixed", 0.02, 4, 60), ("tall", 0.1, 5, 40),
+])
+def test_sharded_one_exchange_band_and_straddle(kind, tie, nshards, k):
+    """The one-allgather protocol's band test, and its rare two-exchange
+    recovery when a near-tie straddles the band (oracle/sharded_model.py)."""
+    T = _straddle_tableau() if kind == "straddle" else gen.tableau(kind, 48, 32, 23)
+    m, n = T.shape[0] - 1, T.shape[1] - 1
+    grp = _lib.create_group(m, n, nshards)
+    for g in grp:
+        g.upload(T)
+    grp[0].set_tol(ratio_tie=tie)
+    grp[0].set_block(4)
+    st, done = grp[0].run(_lib.RULE_STANDARD, k)
+    o = F64Tableau(T, {"ratio_tie": tie})
+    ost, olog = o.run(0, k)
+    assert grp[0].log().tolist() == olog.tolist()
+    for g in grp:
+        b, c = g.row_begin, g.row_count
+        assert np.array_equal(g.rows(1 + b, c), o.T[1 + b:1 + b + c])
+    if kind == "straddle":
+        assert olog.tolist() == [[1, 0]]
+    for g in reversed(grp):
+        g.close()
