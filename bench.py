@@ -135,6 +135,8 @@ def main():
             raise SystemExit("--gpus N > 1 needs torch.distributed.run with N processes")
         raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
 
+    ndev = _lib.device_count()
+    device = local % ndev if ndev else local     # one rank per GPU; wraps only on smaller boxes
     dist = None
     if world > 1:
         import torch.distributed as dist  # plumbing only: uid exchange, barriers, max
@@ -148,10 +150,10 @@ def main():
         uid = _lib.comm_unique_id() if rank == 0 else None
         box = [uid]
         dist.broadcast_object_list(box, src=0)
-        eng = _lib.create_sharded(m, n, rank, world, box[0], device=local)
+        eng = _lib.create_sharded(m, n, rank, world, box[0], device=device)
         assert (eng.row_begin, eng.row_count) == (rb, re_ - rb)
     else:
-        eng = _lib.Engine(m, n, device=local)
+        eng = _lib.Engine(m, n, device=device)
     eng.set_block(args.block)
     eng.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
     blk = 2048
