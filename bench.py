@@ -104,11 +104,15 @@ def cpu_baseline(seconds_target: float = 15.0) -> dict:
             "seconds_per_pivot": sec_per_pivot}
 
 
-def load_traffic(path: str | None):
+def load_traffic(path: str | None, block: int):
+    """HBM bytes per k_sweep launch measured by scripts/hbm_traffic.py (two
+    rocprofv3 --pmc passes on this workload), or None if not measured for
+    this pivots-per-sweep setting."""
     if path and os.path.exists(path):
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        if d.get("block") == block:
+            return d.get("hbm_bytes_per_launch")
     return None
 
 
@@ -191,7 +195,7 @@ def main():
     local_rows = (re_ - rb) + 1
     sweep_b = sweep_bytes(local_rows, n, args.block)
     achieved = sweep_b / (upd_avg_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic_json) if world == 1 else None
+    traffic = load_traffic(args.traffic_json, args.block) if world == 1 else None
     out = {
         "metric": METRIC,
         "value": lp_pps * world,

@@ -114,6 +114,7 @@ struct Args {
     int pad;
     lp_tol tol;
     long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
+    unsigned long long *gran;  // k_group summaries: 2 phases x GROUP_MAXBLOCKS x 8 tagged granules
 };
 
 // launch wrappers (kernels.hip).  t = index of the pivot within its group
@@ -128,8 +129,11 @@ hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max);  // nd_max >= ndef
-// one persistent launch selecting up to `count` chained pivots of a group
-hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec);
+// one persistent launch selecting up to `count` chained pivots of a group;
+// seq numbers the launches of a handle (1 .. 2^26-1, then wraps to 1): it tags
+// the launch's summaries so no stale granule can match
+hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
+                        unsigned seq);
 constexpr int GROUP_BLOCKS = 64;   // co-resident workgroups of k_group (<= CUs) ...
 constexpr int GROUP_MAXBLOCKS = 256;
 constexpr int GROUP_ROWS = 64;     // ... raised so a block owns at most this many rows
@@ -146,6 +150,7 @@ __host__ __device__ inline long long group_lds(long long rc, long long ld, long 
 // per-pivot kernels are used instead)
 __host__ __device__ inline long long group_blocks(long long rc, long long ld, int count)
 {
+    if (ld >= 0x7fffffffLL || rc >= 0x7fffffffLL) return 0;   // indices travel as 31 bits
     long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
     if (g < GROUP_BLOCKS) g = GROUP_BLOCKS;
     while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count) > GROUP_LDS_MAX) g *= 2;

@@ -39,21 +39,42 @@ namespace lpk {
 // reductions
 // ---------------------------------------------------------------------------
 
+// Wave-wide minimum in registers: DPP moves (no LDS round trips): two quad
+// permutes and two row rotates reduce each row of 16 lanes, two row
+// broadcasts fold the four rows into lane 63, a readlane makes the result
+// wave-uniform.  Must be called with all 64 lanes active.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ long long dpp64(long long v)
+{
+    const int lo = __builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWS, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(v >> 32), (int)(v >> 32), CTRL, ROWS, 0xf, false);
+    return ((long long)hi << 32) | (unsigned)lo;
+}
+
+template <typename Op>
+__device__ __forceinline__ long long wave_reduce64(long long v, Op op)
+{
+    v = op(v, dpp64<0xB1, 0xf>(v));    // quad_perm [1,0,3,2]
+    v = op(v, dpp64<0x4E, 0xf>(v));    // quad_perm [2,3,0,1]
+    v = op(v, dpp64<0x124, 0xf>(v));   // row_ror:4
+    v = op(v, dpp64<0x128, 0xf>(v));   // row_ror:8   (row of 16 reduced)
+    v = op(v, dpp64<0x142, 0xa>(v));   // row_bcast:15 into rows 1, 3
+    v = op(v, dpp64<0x143, 0xc>(v));   // row_bcast:31 into rows 2, 3
+    const int lo = __builtin_amdgcn_readlane((int)v, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), 63);
+    return ((long long)hi << 32) | (unsigned)lo;
+}
+
 __device__ __forceinline__ double wave_min(double v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+    return __longlong_as_double(wave_reduce64(__double_as_longlong(v), [](long long a, long long b) {
+        return __double_as_longlong(fmin(__longlong_as_double(a), __longlong_as_double(b)));
+    }));
 }
 
 __device__ __forceinline__ long long wave_min_ll(long long v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const long long w = __shfl_xor(v, o, 64);
-        v = w < v ? w : v;
-    }
-    return v;
+    return wave_reduce64(v, [](long long a, long long b) { return b < a ? b : a; });
 }
 
 // block-wide minima; every thread gets the result.  scratch >= 16 entries.
@@ -669,14 +690,22 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
 
 // ---------------------------------------------------------------------------
 // K-group: every selection of one group of chained pivots in ONE persistent
-// launch (single device).  GROUP_BLOCKS co-resident workgroups; block b owns
-// a slice of the constraint rows (ratio test) and a slice of the columns
-// (pivot row, row 0).  Per pivot: entering column (combine of the row-0
-// summaries), ratio test on own rows -> summaries, grid barrier, leaving row
-// (combine of the ratio summaries), pivot row and row 0 on own columns ->
-// summaries, grid barrier.  Data shared across blocks inside the launch is
-// stored write-through (sc1) by drained waves and loaded sc1 after the
-// barrier's agent-scope counter (MI355X_MICROARCH "Valid forms" row 1).
+// launch (single device).  G co-resident single-wave workgroups; block b owns
+// a slice of the constraint rows (at most one per lane: ratio test) and a
+// slice of the columns (pivot row, row 0).  Per pivot two all-to-all
+// exchanges of tiny per-block summaries:
+//   entering column  <- row-0 summaries of every block
+//   ratio test on own rows -> ratio summary
+//   leaving row      <- ratio summaries of every block
+//   pivot row and row 0 on own columns -> row-0 summary
+// A summary travels as tagged 8-byte granules {payload u32, tag u32}, each
+// written by ONE sc1 store; a reader polls the granules of every block with
+// sc1 loads until every tag is the expected one -- the wait and the data are
+// the same round trip (MI355X_MICROARCH price list: granule hand-offs, no
+// counter).  Larger data a phase publishes for the other blocks (pivot-row
+// values, multipliers, row 0) is stored sc1 and drained before the block's
+// granules, and read with sc1 loads only after all granules matched
+// ("Valid forms" row 1: the granules are the flag).
 // Same float64 operations as k_ratio + k_prow; no host round trips.
 // ---------------------------------------------------------------------------
 
@@ -685,38 +714,71 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
 __device__ __forceinline__ void stamp(const Args &A, int t, int k)
 {
     if (A.stamps && blockIdx.x == 0 && threadIdx.x == 0 && t < BMAX)
-        A.stamps[t * 8 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+        A.stamps[t * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
-// grid barrier k (1, 2, ...) of this launch: all blocks must be resident
-__device__ bool grid_barrier(unsigned *ctr, unsigned target, unsigned *timeout_flag, int *s_ok)
+typedef unsigned long long u64;
+constexpr int NRMAX = (GROUP_MAXBLOCKS + GROUP_THREADS - 1) / GROUP_THREADS;
+constexpr int NGR = 5;   // ratio summary: l (2), q (2), i
+constexpr int NGE = 8;   // row-0 summary: l (2), q (2), i, fneg | rule << 31, P[t][0] (2)
+static_assert(GROUP_ROWS <= GROUP_THREADS, "k_group: one own row per lane");
+
+__device__ __forceinline__ unsigned lo32(double d) { return (unsigned)as_ll(d); }
+__device__ __forceinline__ unsigned hi32(double d) { return (unsigned)((u64)as_ll(d) >> 32); }
+__device__ __forceinline__ double mk_d(unsigned lo, unsigned hi)
 {
-    drain_stores();   // every storing wave
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        int ok = 1;
-        while (ld_sc1(ctr) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 26)) {       // bounded: ~seconds, never expected
-                st_sc1(timeout_flag, 1u);
-                ok = 0;
-                break;
+    return as_d((long long)(((u64)hi << 32) | lo));
+}
+__device__ __forceinline__ unsigned idx32(long long i) { return i == NONE ? 0x7fffffffu : (unsigned)i; }
+__device__ __forceinline__ long long un_idx(unsigned w) { return w == 0x7fffffffu ? NONE : (long long)w; }
+
+// the summary of pivot t, phase ph (0 ratio, 1 row 0) of launch seq
+__device__ __forceinline__ unsigned gtag(unsigned seq, int t, int ph)
+{
+    return seq * (2 * BMAX) + 2 * t + ph;
+}
+
+// lanes 0..n-1 store word[lane] of this block's summary (after the drain)
+__device__ __forceinline__ void publish(u64 *slot, unsigned tag, unsigned w, int n)
+{
+    drain_stores();
+    if ((int)threadIdx.x < n) st_sc1(&slot[threadIdx.x], ((u64)tag << 32) | w);
+}
+
+// every block's summary, lane l holding blocks l + 64k; polls until every
+// granule carries `tag`.  Bounded (a never-expected timeout flags the ctl).
+template <int NR, int NG>
+__device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[NR][NG],
+                       unsigned *timeout_flag)
+{
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const unsigned bb = threadIdx.x + k * GROUP_THREADS;
+            if (bb < G) {
+#pragma unroll
+                for (int g = 0; g < NG; ++g) {
+                    const u64 v = ld_sc1(&base[bb * 8 + g]);
+                    w[k][g] = (unsigned)v;
+                    ok = ok && (unsigned)(v >> 32) == tag;
+                }
             }
         }
-        *s_ok = ok;
+        if (__all(ok)) return true;
+        if (spins > (1u << 22)) {        // seconds: never expected
+            st_sc1(timeout_flag, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
-    __syncthreads();
-    return *s_ok != 0;
 }
 
-// combine of G per-block summaries, loaded once into registers (summary
-// b = tid + k*blockDim, k < NR): two-pass semantics of the oracle.  Returns
-// the winning summary's candidate, or -1 - b when summary b is the first
-// inside the band but its own candidate is not (rare: rescan b's slice).
-constexpr int NR = (GROUP_MAXBLOCKS + GROUP_THREADS - 1) / GROUP_THREADS;
-
+// combine of G per-block summaries held in registers (summary b = lane + 64k):
+// two-pass semantics of the oracle.  Returns the winning summary's candidate,
+// or -1 - b when summary b is the first inside the band but its own candidate
+// is not (rare: rescan b's slice).
+template <int NR>
 __device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[NR],
                                     const double (&q)[NR], unsigned G, double thr, long long *sl,
                                     long long *s_sel)
@@ -737,17 +799,19 @@ __device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[
     return s_sel[0];
 }
 
-constexpr int IPL = 4;   // own rows / columns per lane kept in registers
+constexpr int IPL = 4;   // own columns per lane kept in registers
+constexpr int CH = 8;    // deferred pivots applied per chunk (loads issued together)
 
-__global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int count, int from_erec)
+// NR = summaries per lane (G <= 64 NR)
+template <int NR>
+__global__ void __launch_bounds__(GROUP_THREADS)
+k_group(Args A, int grp, int count, int from_erec, unsigned seq)
 {
     __shared__ double sd[16];
     __shared__ long long sl[16];
     __shared__ long long sR[BMAX];     // local pivot rows of this group
     __shared__ double sPc[BMAX];       // P[s][C] for the current entering column
     __shared__ double sMr[BMAX];       // M[R][s] for the current leaving row
-    __shared__ double s_q;
-    __shared__ int s_ok;
     __shared__ long long s_sel[2];
     // dynamic LDS: this block's rows' multipliers, its columns' pivot-row
     // slices and its slices of row 0 / column 0 (own data never leaves LDS
@@ -757,23 +821,22 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
     const unsigned G = gridDim.x, b = blockIdx.x;
     const int tid = threadIdx.x;
     const int nth = blockDim.x;
-    if (b == 0 && tid == 0) {          // the other parity's launch and sweep are complete
-        ctl->bar[grp ^ 1] = 0;
-        ctl->ndef[grp ^ 1] = 0;
-    }
+    if (b == 0 && tid == 0) ctl->ndef[grp ^ 1] = 0;   // the other parity's sweep is complete
     if (ld_sc1(&ctl->status) != LP_PIVOTED) return;
-    unsigned *bar = &ctl->bar[grp];
-    unsigned nbar = 0;
-    const long long rpb = (A.rc + G - 1) / G;               // rows per block
+    u64 *grR = A.gran;                         // ratio summaries [G][8]
+    u64 *grE = A.gran + GROUP_MAXBLOCKS * 8;   // row-0 summaries [G][8]
+    const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= nth)
     const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
     const long long cpb = (A.ld + G - 1) / G;               // columns per block
     const long long jc0 = b * cpb, jc1 = min(jc0 + cpb, A.ld);
-    double *lM = dyn;                        // [rpb][count]
+    double *lM = dyn;                        // [count][rpb] (pivot-major: lanes read consecutive words)
     double *lP = lM + rpb * count;           // [count][cpb]
     double *l0 = lP + count * cpb;           // [cpb]  row 0 slice
     double *lc = l0 + cpb;                   // [rpb]  column 0 slice
+    const long long li = lr0 + tid;          // this lane's own row
+    const bool own = li < lr1;
     for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = A.row0[j];
-    for (long long li = lr0 + tid; li < lr1; li += nth) lc[li - lr0] = A.col0[li];
+    if (own) lc[tid] = A.col0[li];
     const long long cap = ctl->cap;
     const int mode = ctl->mode;
     // counters live in registers for the launch (block 0 publishes them)
@@ -789,14 +852,12 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
     int status = LP_PIVOTED;
     int pending = -1;                 // pivot whose column-0 update is still due
     long long pendR = -1;
+    double p0 = 0.0;                  // its P[.][0]
     __syncthreads();
     for (int t = 0; t < count; ++t) {
         stamp(A, t, 0);
-        // ---- entering column (+ the previous pivot's column-0 update, whose
-        //      P[.][0] load shares the round trip with the summaries)
+        // ---- entering column
         long long C;
-        double p0 = 0.0;
-        if (pending >= 0) p0 = ld_sc1(&A.P[pending * A.ld]);
         if (t == 0 && !from_erec) {
             C = ld_sc1(&ctl->c) + 1;
         } else {
@@ -805,24 +866,50 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
             long long ei[NR];
             long long ef = NONE;
             double emin = INFINITY;
+            if (t == 0) {      // previous launch's summaries (kernel boundary: plain data)
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const unsigned bb = tid + k * nth;
-                el[k] = INFINITY;
-                eq[k] = 0.0;
-                ei[k] = NONE;
-                if (bb < G) {
-                    el[k] = ld_sc1(&A.erec[bb].l);
-                    ei[k] = ld_sc1(&A.erec[bb].i);
-                    eq[k] = ld_sc1(&A.erec[bb].q);
-                    const long long f = ld_sc1(&A.erec[bb].fneg);
-                    ef = f < ef ? f : ef;
-                    emin = fmin(emin, el[k]);
+                for (int k = 0; k < NR; ++k) {
+                    const unsigned bb = tid + k * nth;
+                    el[k] = INFINITY;
+                    eq[k] = 0.0;
+                    ei[k] = NONE;
+                    if (bb < G) {
+                        el[k] = ld_sc1(&A.erec[bb].l);
+                        ei[k] = ld_sc1(&A.erec[bb].i);
+                        eq[k] = ld_sc1(&A.erec[bb].q);
+                        const long long f = ld_sc1(&A.erec[bb].fneg);
+                        ef = f < ef ? f : ef;
+                        emin = fmin(emin, el[k]);
+                    }
                 }
+                const long long rr = tid == 0 ? ld_sc1(&A.erec[0].rule) : 0;
+                rule = (int)__shfl(rr, 0, 64);
+            } else {
+                unsigned w[NR][NGE];
+                if (!gather<NR, NGE>(grE, G, gtag(seq, t - 1, 1), w, &ctl->bar_timeout)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+#pragma unroll
+                for (int k = 0; k < NR; ++k) {
+                    const unsigned bb = tid + k * nth;
+                    el[k] = INFINITY;
+                    eq[k] = 0.0;
+                    ei[k] = NONE;
+                    if (bb < G) {
+                        el[k] = mk_d(w[k][0], w[k][1]);
+                        eq[k] = mk_d(w[k][2], w[k][3]);
+                        ei[k] = un_idx(w[k][4]);
+                        const long long f = un_idx(w[k][5] & 0x7fffffffu);
+                        ef = f < ef ? f : ef;
+                        emin = fmin(emin, el[k]);
+                    }
+                }
+                // block 0's summary (lane 0) carries the rule and P[t-1][0]
+                rule = (int)((unsigned)__builtin_amdgcn_readfirstlane(w[0][5]) >> 31);
+                p0 = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
+                          __builtin_amdgcn_readfirstlane(w[0][7]));
             }
-            // the rule (stall switch) arrives in block 0's summary, same round trip
-            long long rr = tid == 0 ? ld_sc1(&A.erec[0].rule) : 0;
-            rule = (int)__shfl(rr, 0, 64);
             if (capped) {
                 C = NONE;
             } else if (rule == LP_RULE_MIN_INDEX) {
@@ -845,91 +932,96 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
             }
             if (C == NONE) status = capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
+        stamp(A, t, 1);
         if (pending >= 0) {
-            for (long long li = lr0 + tid; li < lr1; li += nth) {
-                const long long k = li - lr0;
-                const double c0 = upd(li, pendR, lM[k * count + pending], p0, lc[k]);
-                lc[k] = c0;
+            if (own) {
+                const double c0 = upd(li, pendR, lM[pending * rpb + tid], p0, lc[tid]);
+                lc[tid] = c0;
                 st_sc1(&A.col0[li], c0);
             }
             pending = -1;
         }
         if (status != LP_PIVOTED) break;
-        stamp(A, t, 1);
+        stamp(A, t, 2);
         // ---- ratio test over own rows; M[t] of own rows.  The tableau column
-        //      loads are issued before the cross-block loads (one round trip).
-        double av[IPL];
-#pragma unroll
-        for (int k = 0; k < IPL; ++k) {
-            const long long li = lr0 + tid + k * nth;
-            av[k] = li < lr1 ? A.T[li * A.ld + C] : 0.0;
-        }
+        //      load is issued before the cross-block loads (one round trip).
+        double a = own ? A.T[li * A.ld + C] : 0.0;
         if (tid < t) sPc[tid] = ld_sc1(&A.P[tid * A.ld + C]);
         if (tid == 0) {
             if (b == 0) st_sc1(&ctl->c, C - 1);
             if (C >= jc0 && C < jc1) st_sc1(&A.M[t], l0[C - jc0]);   // row 0's multiplier
         }
         __syncthreads();
-        double lbest = INFINITY;
-        auto ratio_row = [&](long long li, double a) {
-            const long long k = li - lr0;
-            for (int s2 = 0; s2 < t; ++s2) a = upd(li, sR[s2], lM[k * count + s2], sPc[s2], a);
-            lM[k * count + t] = a;
-            st_sc1(&A.M[li * BMAX + t], a);
-            bool ok;
-            const double q = row_ratio(a, lc[k], A.tol, ok);
-            if (ok) lbest = fmin(lbest, q);
-        };
+        stamp(A, t, 3);
+        for (int s0 = 0; s0 < t; s0 += CH) {
+            long long rr[CH];
+            double pc[CH], mm[CH];
 #pragma unroll
-        for (int k2 = 0; k2 < IPL; ++k2) {
-            const long long li = lr0 + tid + k2 * nth;
-            if (li < lr1) ratio_row(li, av[k2]);
+            for (int u = 0; u < CH; ++u) {
+                const int s = min(s0 + u, count - 1);
+                rr[u] = sR[s];
+                pc[u] = sPc[s];
+                mm[u] = lM[s * rpb + min((long long)tid, rpb - 1)];
+            }
+#pragma unroll
+            for (int u = 0; u < CH; ++u)
+                if (s0 + u < t) a = upd(li, rr[u], mm[u], pc[u], a);
         }
-        for (long long li = lr0 + tid + IPL * nth; li < lr1; li += nth)
-            ratio_row(li, A.T[li * A.ld + C]);
-        const double lb = block_min(lbest, sd);
+        double qown = 0.0;
+        bool okown = false;
+        if (own) {
+            lM[t * rpb + tid] = a;
+            st_sc1(&A.M[li * BMAX + t], a);
+            qown = row_ratio(a, lc[tid], A.tol, okown);
+        }
+        const double lb = block_min(own && okown ? qown : INFINITY, sd);
+        stamp(A, t, 4);
         long long ib = NONE;
         double qb = 0.0;
         if (lb < INFINITY) {
+            // own rows are lanes in row order: the first row inside the band
+            // is the lowest lane that has one
             const double thr = tie_band(lb, A.tol.ratio_tie);
-            long long mine = NONE;
-            double qmine = 0.0;
-            for (long long li = lr0 + tid; li < lr1; li += nth) {
-                bool ok;
-                const double q = row_ratio(lM[(li - lr0) * count + t], lc[li - lr0], A.tol, ok);
-                if (ok && q <= thr) { mine = li; qmine = q; break; }
-            }
-            ib = block_min_ll(mine, sl);
-            if (mine == ib) s_q = qmine;
-            __syncthreads();
-            qb = s_q;
+            const u64 mask = __ballot(own && okown && qown <= thr);
+            const int f = __builtin_ctzll(mask);
+            ib = lr0 + f;
+            qb = mk_d(__builtin_amdgcn_readlane(lo32(qown), f), __builtin_amdgcn_readlane(hi32(qown), f));
         }
-        if (tid == 0) {
-            st_sc1(&A.rec[b].l, lb);
-            st_sc1(&A.rec[b].i, ib);
-            st_sc1(&A.rec[b].q, qb);
+        {
+            unsigned wv = idx32(ib);
+            if (tid == 0) wv = lo32(lb);
+            else if (tid == 1) wv = hi32(lb);
+            else if (tid == 2) wv = lo32(qb);
+            else if (tid == 3) wv = hi32(qb);
+            publish(&grR[b * 8], gtag(seq, t, 0), wv, NGR);
         }
-        stamp(A, t, 2);
-        if (!grid_barrier(bar, G * ++nbar, &ctl->bar_timeout, &s_ok)) { status = LP_DEVICE_ERROR; break; }
-        stamp(A, t, 3);
+        stamp(A, t, 5);
 
-        // ---- leaving row (combine the ratio summaries: one load each)
+        // ---- leaving row (combine the ratio summaries)
         double rl[NR], rq[NR];
         long long ri[NR];
         double rmin = INFINITY;
+        {
+            unsigned w[NR][NGR];
+            if (!gather<NR, NGR>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
 #pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const unsigned bb = tid + k * nth;
-            rl[k] = INFINITY;
-            rq[k] = 0.0;
-            ri[k] = NONE;
-            if (bb < G) {
-                rl[k] = ld_sc1(&A.rec[bb].l);
-                ri[k] = ld_sc1(&A.rec[bb].i);
-                rq[k] = ld_sc1(&A.rec[bb].q);
-                rmin = fmin(rmin, rl[k]);
+            for (int k = 0; k < NR; ++k) {
+                const unsigned bb = tid + k * nth;
+                rl[k] = INFINITY;
+                rq[k] = 0.0;
+                ri[k] = NONE;
+                if (bb < G) {
+                    rl[k] = mk_d(w[k][0], w[k][1]);
+                    rq[k] = mk_d(w[k][2], w[k][3]);
+                    ri[k] = un_idx(w[k][4]);
+                    rmin = fmin(rmin, rl[k]);
+                }
             }
         }
+        stamp(A, t, 6);
         const double g = block_min(rmin, sd);
         if (!(g < INFINITY)) { status = LP_UNBOUNDED; break; }
         const double thr = tie_band(g, A.tol.ratio_tie);
@@ -938,14 +1030,14 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
             const long long bsel = -1 - R;
             const long long r0 = 1 + bsel * rpb, r1 = min(r0 + rpb, A.rows);
             long long mine = NONE;
-            for (long long li = r0 + tid; li < r1; li += nth) {
+            for (long long lj = r0 + tid; lj < r1; lj += nth) {
                 bool ok;
-                const double q = row_ratio(ld_sc1(&A.M[li * BMAX + t]), ld_sc1(&A.col0[li]), A.tol, ok);
-                if (ok && q <= thr) { mine = li; break; }
+                const double q = row_ratio(ld_sc1(&A.M[lj * BMAX + t]), ld_sc1(&A.col0[lj]), A.tol, ok);
+                if (ok && q <= thr) { mine = lj; break; }
             }
             R = block_min_ll(mine, sl);
         }
-        stamp(A, t, 4);
+        stamp(A, t, 7);
         // ---- pivot row on own columns, row 0 on own columns.  Tableau row
         //      loads first, then the cross-block loads (one round trip).
         double xv[IPL];
@@ -958,13 +1050,35 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
         if (tid == 0) sR[t] = R;
         const double f0 = ld_sc1(&A.M[t]);
         __syncthreads();
-        const double a = sMr[t];
+        stamp(A, t, 8);
+        const double av = sMr[t];
+        // deferred pivots 0..t-1 of the group on the own columns, CH at a time
+        auto chain = [&](double (&x)[IPL], long long kbase) {
+            for (int s0 = 0; s0 < t; s0 += CH) {
+                long long rr[CH];
+                double mr[CH], pv[CH][IPL];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int s = min(s0 + u, count - 1);
+                    rr[u] = sR[s];
+                    mr[u] = sMr[s];
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k)
+                        pv[u][k] = lP[s * cpb + min(kbase + k * nth, cpb - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (s0 + u < t) {
+#pragma unroll
+                        for (int k = 0; k < IPL; ++k) x[k] = upd(R, rr[u], mr[u], pv[u][k], x[k]);
+                    }
+            }
+        };
         double vmin = INFINITY, v0 = 0.0;
         long long fneg = NONE;
-        auto prow_col = [&](long long j, double x) {
+        auto finish_col = [&](long long j, double x) {
             const long long k = j - jc0;
-            for (int s2 = 0; s2 < t; ++s2) x = upd(R, sR[s2], sMr[s2], lP[s2 * cpb + k], x);
-            const double p = (j == C) ? 1.0 : x / a;
+            const double p = (j == C) ? 1.0 : x / av;
             lP[t * cpb + k] = p;
             st_sc1(&A.P[t * A.ld + j], p);
             const double v = upd(0, -1, f0, p, l0[k]);
@@ -976,12 +1090,28 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
                 if (v < -A.tol.cost && j < fneg) fneg = j;
             }
         };
+        chain(xv, tid);
 #pragma unroll
         for (int k2 = 0; k2 < IPL; ++k2) {
             const long long j = jc0 + tid + k2 * nth;
-            if (j < jc1) prow_col(j, xv[k2]);
+            if (j < jc1) finish_col(j, xv[k2]);
         }
-        for (long long j = jc0 + tid + IPL * nth; j < jc1; j += nth) prow_col(j, A.T[R * A.ld + j]);
+        for (long long j0 = jc0 + IPL * nth; j0 < jc1; j0 += IPL * nth) {   // wide slices
+            double x2[IPL];
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                const long long j = j0 + tid + k * nth;
+                x2[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
+            }
+            chain(x2, j0 - jc0 + tid);
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                const long long j = j0 + tid + k * nth;
+                if (j < jc1) finish_col(j, x2[k]);
+            }
+        }
+        __syncthreads();
+        stamp(A, t, 9);
         // row-0 summary of own columns
         const double el = block_min(vmin, sd);
         const long long efn = block_min_ll(fneg, sl);
@@ -996,10 +1126,11 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
                 if (j >= 1 && j <= A.n && v <= ethr) { mine = j; vmine = v; break; }
             }
             ei = block_min_ll(mine, sl);
-            if (mine == ei) s_q = vmine;
-            __syncthreads();
-            eq = s_q;
+            const u64 mask = __ballot(mine == ei);
+            const int f = __builtin_ctzll(mask);
+            eq = mk_d(__builtin_amdgcn_readlane(lo32(vmine), f), __builtin_amdgcn_readlane(hi32(vmine), f));
         }
+        stamp(A, t, 10);
         if (b == 0 && tid == 0) {     // column 0 is in block 0's slice: v0 = new row0[0]
             const long long rglob = R - 1 + A.rb;
             st_sc1(&A.dR[t], R);
@@ -1022,28 +1153,45 @@ __global__ void __launch_bounds__(GROUP_THREADS) k_group(Args A, int grp, int co
                 st_sc1(&ctl->stuck, stuck);
                 st_sc1(&ctl->rule, rule);
             }
-            st_sc1(&A.erec[0].rule, (long long)rule);
         }
-        if (tid == 0) {
-            st_sc1(&A.erec[b].l, el);
-            st_sc1(&A.erec[b].i, ei);
-            st_sc1(&A.erec[b].q, eq);
-            st_sc1(&A.erec[b].fneg, efn);
+        rule = __builtin_amdgcn_readfirstlane(rule);   // block 0 lane 0 may have switched it
+        const double p0n = b == 0 ? lP[t * cpb] : 0.0;     // P[t][0] (column 0 is block 0's)
+        if (t == count - 1) {         // the next launch reads plain summaries
+            if (tid == 0) {
+                st_sc1(&A.erec[b].l, el);
+                st_sc1(&A.erec[b].i, ei);
+                st_sc1(&A.erec[b].q, eq);
+                st_sc1(&A.erec[b].fneg, efn);
+                if (b == 0) st_sc1(&A.erec[0].rule, (long long)rule);
+            }
+        }
+        {
+            unsigned wv = 0;
+            if (tid == 0) wv = lo32(el);
+            else if (tid == 1) wv = hi32(el);
+            else if (tid == 2) wv = lo32(eq);
+            else if (tid == 3) wv = hi32(eq);
+            else if (tid == 4) wv = idx32(ei);
+            else if (tid == 5) wv = (idx32(efn) & 0x7fffffffu) | ((unsigned)rule << 31);
+            else if (tid == 6) wv = lo32(p0n);
+            else if (tid == 7) wv = hi32(p0n);
+            publish(&grE[b * 8], gtag(seq, t, 1), wv, NGE);
         }
         ++npiv;
-        stamp(A, t, 5);
-        if (!grid_barrier(bar, G * ++nbar, &ctl->bar_timeout, &s_ok)) { status = LP_DEVICE_ERROR; break; }
-        stamp(A, t, 6);
+        stamp(A, t, 11);
         pending = t;
         pendR = R;
-        stamp(A, t, 7);
     }
-    // the last pivot's column-0 update (P[.][0] is published: barrier passed)
+    // the last pivot's column-0 update: P[pending][0] arrives in block 0's
+    // row-0 summary
     if (pending >= 0) {
-        const double p0 = ld_sc1(&A.P[pending * A.ld]);
-        for (long long li = lr0 + tid; li < lr1; li += nth) {
-            const long long k = li - lr0;
-            st_sc1(&A.col0[li], upd(li, pendR, lM[k * count + pending], p0, lc[k]));
+        unsigned w[NR][NGE];
+        if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout)) {
+            const double pl = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
+                                   __builtin_amdgcn_readfirstlane(w[0][7]));
+            if (own) st_sc1(&A.col0[li], upd(li, pendR, lM[pending * rpb + tid], pl, lc[tid]));
+        } else {
+            status = LP_DEVICE_ERROR;
         }
     }
     if (b == 0 && tid == 0 && status != LP_PIVOTED) st_sc1(&ctl->status, status);
@@ -1245,14 +1393,23 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max)
     return hipGetLastError();
 }
 
-hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec)
+hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
+                        unsigned seq)
 {
     if (count < 1 || count > BMAX) return hipErrorInvalidValue;
     const long long g = group_blocks(A.rc, A.ld, count);
     if (g == 0) return hipErrorInvalidValue;
     const size_t lds = (size_t)group_lds(A.rc, A.ld, g, count);
-    hipLaunchKernelGGL(k_group, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp, count,
-                       from_erec);
+    const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
+    if (nr <= 1)
+        hipLaunchKernelGGL(k_group<1>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp,
+                           count, from_erec, seq);
+    else if (nr <= 2)
+        hipLaunchKernelGGL(k_group<2>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp,
+                           count, from_erec, seq);
+    else
+        hipLaunchKernelGGL(k_group<NRMAX>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A,
+                           grp, count, from_erec, seq);
     return hipGetLastError();
 }
 

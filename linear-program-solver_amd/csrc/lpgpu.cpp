@@ -44,6 +44,8 @@ struct lp_handle {
     int block = 16;                 // pivots deferred into one sweep (1..BMAX)
     bool persistent = true;         // single device: one k_group launch per group
     long long *stamps = nullptr;    // diagnostic phase clocks (LPGPU_STAMPS=1)
+    unsigned long long *gran = nullptr;  // k_group summaries (tagged granules)
+    unsigned gseq = 0;              // k_group launches so far (tags their summaries)
     bool eager_ok = false;          // row0/col0 mirror the stored tableau
     Ctl *ctl = nullptr;
     Ctl *hctl = nullptr;            // pinned mirror
@@ -192,6 +194,7 @@ static Args args_of(const lp_handle *h)
     A.pad = 0;
     A.tol = h->tol;
     A.stamps = h->stamps;
+    A.gran = h->gran;
     return A;
 }
 
@@ -231,8 +234,8 @@ static int alloc_handle(lp_handle *h)
         h->persistent = std::strcmp(sel, "kernels") != 0;
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
-            HCHK(h, hipMalloc(&h->stamps, lpk::BMAX * 8 * sizeof(long long)));
-            HCHK(h, hipMemset(h->stamps, 0, lpk::BMAX * 8 * sizeof(long long)));
+            HCHK(h, hipMalloc(&h->stamps, lpk::BMAX * 16 * sizeof(long long)));
+            HCHK(h, hipMemset(h->stamps, 0, lpk::BMAX * 16 * sizeof(long long)));
         }
     HCHK(h, hipSetDevice(h->dev));
     if (!h->s) HCHK(h, hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
@@ -243,6 +246,9 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMemsetAsync(h->P, 0, (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
     HCHK(h, hipMalloc(&h->M, (size_t)lpk::BMAX * h->rows * sizeof(double)));
     HCHK(h, hipMemsetAsync(h->M, 0, (size_t)lpk::BMAX * h->rows * sizeof(double), h->s));
+    const size_t gbytes = 2 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
+    HCHK(h, hipMalloc(&h->gran, gbytes));
+    HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
     HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));
     HCHK(h, hipMemsetAsync(h->row0, 0, (size_t)h->ld * sizeof(double), h->s));
     HCHK(h, hipMalloc(&h->col0, (size_t)h->rows * sizeof(double)));
@@ -408,6 +414,7 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->dC) (void)hipFree(h->dC);
     if (h->erec) (void)hipFree(h->erec);
     if (h->stamps) (void)hipFree(h->stamps);
+    if (h->gran) (void)hipFree(h->gran);
     if (h->ctl) (void)hipFree(h->ctl);
     if (h->hctl) (void)hipHostFree(h->hctl);
     if (h->log) (void)hipFree(h->log);
@@ -684,7 +691,8 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             // one persistent selection launch + one sweep per group
             for (int64_t k = 0; k < b; k += B) {
                 const int cnt = (int)std::min<int64_t>(B, b - k);
-                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0));
+                h->gseq = h->gseq % ((1u << 26) - 1) + 1;
+                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0, h->gseq));
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
                 chained = true;
@@ -825,6 +833,6 @@ extern "C" int lp_update_time(lp_handle *h, double *ms, int64_t *launches)
 extern "C" int lpdiag_stamps(lp_handle *h, long long *out)
 {
     if (!h->stamps) return LP_BAD_ARG;
-    HCHK(h, hipMemcpy(out, h->stamps, lpk::BMAX * 8 * sizeof(long long), hipMemcpyDeviceToHost));
+    HCHK(h, hipMemcpy(out, h->stamps, lpk::BMAX * 16 * sizeof(long long), hipMemcpyDeviceToHost));
     return LP_PIVOTED;
 }

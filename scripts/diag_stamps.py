@@ -14,14 +14,16 @@ e.upload(T)
 e.set_block(16)
 e.run(0, 64)
 e.run(0, 16)
-buf = (C.c_longlong * (32 * 8))()
+buf = (C.c_longlong * (32 * 16))()
 assert e.lib.lpdiag_stamps(e.h, buf) == 0
-names = ["enter", "ratio", "bar1", "leave", "prow", "bar2", "col0"]
+# stamp k marks the END of segment names[k-1]; segment 13 runs to the next pivot's stamp 0
+names = ["enter", "col0", "rload", "rcomp", "rpub", "gathR", "leave",
+         "pload", "pcomp", "esum", "epub", "tail"]
 rows = []
-for t in range(16):
-    st = [buf[t * 8 + k] for k in range(8)]
-    d = [(st[k + 1] - st[k]) * 10 / 1000 for k in range(7)]   # 100 MHz ticks -> us
+for t in range(15):
+    st = [buf[t * 16 + k] for k in range(len(names))] + [buf[(t + 1) * 16]]
+    d = [(st[k + 1] - st[k]) * 10 / 1000 for k in range(len(names))]   # 100 MHz ticks -> us
     rows.append(d)
-    print(t, " ".join(f"{n}={x:5.2f}" for n, x in zip(names, d)))
-avg = [sum(r[k] for r in rows[1:]) / (len(rows) - 1) for k in range(7)]
-print("avg", " ".join(f"{n}={x:5.2f}" for n, x in zip(names, avg)), "sum", round(sum(avg), 2))
+    print(t, " ".join(f"{n}={x:4.2f}" for n, x in zip(names, d)))
+avg = [sum(r[k] for r in rows[1:]) / (len(rows) - 1) for k in range(len(names))]
+print("avg", " ".join(f"{n}={x:4.2f}" for n, x in zip(names, avg)), "sum", round(sum(avg), 2))

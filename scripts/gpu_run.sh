@@ -18,6 +18,7 @@ run() {
 for step in "$@"; do
     case "$step" in
         pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider ;;
+        pytestx) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         benchq) run benchq 300 python bench.py --no-cpu-baseline ;;
@@ -40,6 +41,18 @@ for step in "$@"; do
         prof)
             export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$PWD/bench.py" --steps 200 --no-cpu-baseline ;;
+        stamps)
+            run stamps 300 python scripts/diag_stamps.py ;;
+        pmc)
+            export TMPDIR=/tmp
+            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
+            run pmc_json 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" --block 16
+            # later steps of this call (bench) report it as roofline.traffic
+            if [ -f "$OUT/hbm_traffic.json" ]; then cp "$OUT/hbm_traffic.json" profiles/r01/hbm_traffic.json; fi ;;
+        proffinal)
+            export TMPDIR=/tmp
+            run rocprof_final 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_final" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -1,0 +1,73 @@
+"""HBM bytes per k_sweep launch from two rocprofv3 --pmc passes.
+
+FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950 (TCC slots), so
+scripts/gpu_run.sh runs bench.py twice under rocprofv3, once per counter.
+Both counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
+wide coalesced streaming read, so it is doubled (MI355X_MICROARCH.md §HBM).
+
+usage: python scripts/hbm_traffic.py FETCH_DIR WRITE_DIR OUT_JSON --block B
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    vals: dict[str, float] = {}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel not in row.get("Kernel_Name", ""):
+                    continue
+                if row.get("Counter_Name") != counter:
+                    continue
+                key = f + ":" + row.get("Dispatch_Id", str(len(vals)))
+                vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("out")
+    ap.add_argument("--block", type=int, default=16)
+    ap.add_argument("--kernel", default="k_sweep")
+    a = ap.parse_args()
+    import bench
+    fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
+    write = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
+    if not fetch or not write:
+        raise SystemExit(f"no {a.kernel} dispatches with counters")
+    f_kib, w_kib = statistics.mean(fetch), statistics.mean(write)
+    hbm = (2.0 * f_kib + w_kib) * 1024.0
+    alg = bench.sweep_bytes(bench.ROWS_PER_GPU + 1, bench.NCOLS, a.block)
+    out = {
+        "kernel": f"{a.kernel}<{a.block}>",
+        "workload": "cfg3 4096x8192 G_mixed seed 3 (bench.py, 1 GPU)",
+        "block": a.block,
+        "dispatches": [len(fetch), len(write)],
+        "FETCH_SIZE_KiB_mean": f_kib,
+        "WRITE_SIZE_KiB_mean": w_kib,
+        "correction": "FETCH_SIZE x2 (gfx950 reports half of a wide coalesced read), KiB x1024",
+        "hbm_bytes_per_launch": hbm,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": hbm / alg,
+    }
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
