@@ -121,7 +121,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1024)
     ap.add_argument("--warmup", type=int, default=32)
-    ap.add_argument("--block", type=int, default=16,
+    ap.add_argument("--block", type=int, default=32,
                     help="pivots deferred into one sweep of the tableau (1 = eager)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

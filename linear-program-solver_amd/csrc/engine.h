@@ -38,12 +38,20 @@ constexpr int BMAX = 32;           // most pivots deferred into one sweep
 constexpr int RATIO_THREADS = 256;
 constexpr int RATIO_CHUNK = 256;   // rows per ratio block (one per thread)
 constexpr int PROW_THREADS = 256;  // columns per pivot-row block (one per thread)
-constexpr int SWEEP_ROWS = 64;     // rows per sweep block
-constexpr int SWEEP_UNROLL = 4;    // rows in flight per wave
+
 constexpr int ENTER_THREADS = 1024;
 constexpr int SLOT_HDR = 8;        // doubles of header in front of an exchanged row
 
 constexpr long long NONE = 0x7fffffffffffffffLL;
+
+// multipliers are stored pivot-major: M[s * rows + li] is the value of
+// (local row li, dC[s]) just before pivot s, so one pivot's multipliers of
+// consecutive rows are contiguous (coalesced stores, wide scalar loads)
+__host__ __device__ inline long long mi(long long rows, long long li, long long s)
+{
+    return s * rows + li;
+}
+constexpr int M_PAD = 64;          // doubles after each parity's M (wide loads past the last row)
 
 // Device-resident control block: the pivot loop's whole state lives here so
 // batches of pivots are enqueued without host round trips.
@@ -93,7 +101,7 @@ struct Args {
     double *T;           // local tableau: row 0 + local constraint rows
     double *row0;        // current row 0 (ld doubles)
     double *col0;        // current column 0 of the local rows (rows doubles)
-    double *M;           // rows x BMAX multipliers (row-major: a row's are contiguous)
+    double *M;           // BMAX x rows multipliers, pivot-major (mi())
     double *P;           // BMAX x ld normalised pivot rows
     long long *dR;       // BMAX local pivot rows (-1: another rank's row)
     long long *dC;       // BMAX pivot columns (tableau index)
@@ -115,6 +123,13 @@ struct Args {
     lp_tol tol;
     long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
     unsigned long long *gran;  // k_group summaries: 2 phases x GROUP_MAXBLOCKS x 8 tagged granules
+    // pipelined groups (k_group only): the previous group's pivots are not yet
+    // in T (its sweep runs concurrently); lag = 1 applies them on the fly first
+    const double *Pp;    // previous group's P (BMAX x ld)
+    const double *Mp;    // previous group's M
+    const long long *dRp;// previous group's local pivot rows
+    int lag;
+    int pad2;
 };
 
 // launch wrappers (kernels.hip).  t = index of the pivot within its group
@@ -128,34 +143,37 @@ hipError_t launch_ratio(hipStream_t s, const Args &A, int t, int grp, int mode, 
 hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max);  // nd_max >= ndef
+// T_out <- A.T with the group's pivots (T_out == A.T: in place); nd_max >= ndef
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out);
 // one persistent launch selecting up to `count` chained pivots of a group;
 // seq numbers the launches of a handle (1 .. 2^26-1, then wraps to 1): it tags
 // the launch's summaries so no stale granule can match
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq);
+                        unsigned seq, int bmax);
 constexpr int GROUP_BLOCKS = 64;   // co-resident workgroups of k_group (<= CUs) ...
 constexpr int GROUP_MAXBLOCKS = 256;
 constexpr int GROUP_ROWS = 64;     // ... raised so a block owns at most this many rows
 constexpr int GROUP_THREADS = 64;  // one wave: block reductions stay in registers
 constexpr long long GROUP_LDS_MAX = 96 * 1024;
 // dynamic LDS of one k_group block (own multipliers, pivot-row slices, row 0
-// and column 0 slices)
-__host__ __device__ inline long long group_lds(long long rc, long long ld, long long g, int count)
+// and column 0 slices; with a lagging previous group of up to `count` pivots
+// its multipliers and pivot-row slices too)
+__host__ __device__ inline long long group_lds(long long rc, long long ld, long long g, int count,
+                                               int lag)
 {
     const long long rpb = (rc + g - 1) / g, cpb = (ld + g - 1) / g;
-    return (rpb * count + count * cpb + cpb + rpb) * 8;
+    return ((rpb * count + count * cpb) * (lag ? 2 : 1) + cpb + rpb) * 8;
 }
 // workgroups of k_group for this shape, 0 if its LDS would not fit (the
 // per-pivot kernels are used instead)
-__host__ __device__ inline long long group_blocks(long long rc, long long ld, int count)
+__host__ __device__ inline long long group_blocks(long long rc, long long ld, int count, int lag)
 {
     if (ld >= 0x7fffffffLL || rc >= 0x7fffffffLL) return 0;   // indices travel as 31 bits
     long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
     if (g < GROUP_BLOCKS) g = GROUP_BLOCKS;
-    while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count) > GROUP_LDS_MAX) g *= 2;
+    while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX) g *= 2;
     if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
-    return group_lds(rc, ld, g, count) > GROUP_LDS_MAX ? 0 : g;
+    return group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX ? 0 : g;
 }
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
 hipError_t launch_resume(hipStream_t s, const Args &A);

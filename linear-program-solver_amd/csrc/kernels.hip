@@ -33,6 +33,8 @@
 // aligned).
 #include "engine.h"
 
+#include <cstdlib>
+
 namespace lpk {
 
 // ---------------------------------------------------------------------------
@@ -172,7 +174,7 @@ __device__ __forceinline__ double upd(long long li, long long R, double f, doubl
 __device__ double current(const Args &A, int t, long long li, long long j, double x)
 {
     for (int s = 0; s < t; ++s)
-        x = upd(li, A.dR[s], A.M[li * BMAX + s], A.P[s * A.ld + j], x);
+        x = upd(li, A.dR[s], A.M[mi(A.rows, li, s)], A.P[s * A.ld + j], x);
     return x;
 }
 
@@ -185,7 +187,7 @@ __device__ __forceinline__ double current_col(const Args &A, int t, long long li
     if constexpr (TP > 0) {
         double mv[TP];
 #pragma unroll
-        for (int s = 0; s < TP; ++s) mv[s] = A.M[li * BMAX + s];
+        for (int s = 0; s < TP; ++s) mv[s] = A.M[mi(A.rows, li, s)];
 #pragma unroll
         for (int s = 0; s < TP; ++s)
             if (s < t) x = upd(li, sR[s], mv[s], sPc[s], x);
@@ -205,7 +207,7 @@ __device__ __forceinline__ double current_row(const Args &A, int t, long long R,
         for (int s = 0; s < TP; ++s) pv[s] = A.P[s * A.ld + j];
 #pragma unroll
         for (int s = 0; s < TP; ++s)
-            if (s < t) x = upd(R, A.dR[s], A.M[R * BMAX + s], pv[s], x);
+            if (s < t) x = upd(R, A.dR[s], A.M[mi(A.rows, R, s)], pv[s], x);
     }
     return x;
 }
@@ -417,7 +419,7 @@ k_ratio(Args A, int t, int grp, int mode, int from_erec, long long check_row)
         sR[threadIdx.x] = A.dR[threadIdx.x];
         sPc[threadIdx.x] = A.P[threadIdx.x * A.ld + C];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.M[t] = A.row0[C];   // row 0's multiplier
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.M[mi(A.rows, 0, t)] = A.row0[C];   // row 0's multiplier
     __syncthreads();
 
     const long long li0 = 1 + (long long)blockIdx.x * RATIO_CHUNK;
@@ -427,7 +429,7 @@ k_ratio(Args A, int t, int grp, int mode, int from_erec, long long check_row)
     double q = 0.0;
     if (li < li1) {
         const double a = current_col<TP>(A, t, li, A.T[li * A.ld + C], sR, sPc);
-        A.M[li * BMAX + t] = a;
+        A.M[mi(A.rows, li, t)] = a;
         q = row_ratio(a, A.col0[li], A.tol, ok);
     }
     const double lb = block_min(ok ? q : INFINITY, sd);
@@ -540,7 +542,7 @@ __global__ void k_gather(Args A, int t)
     const long long C = ctl->c + 1;
     for (long long li = blockIdx.x * (long long)blockDim.x + threadIdx.x; li < A.rows;
          li += (long long)gridDim.x * blockDim.x)
-        A.M[li * BMAX + t] = li == 0 ? A.row0[C] : current(A, t, li, C, A.T[li * A.ld + C]);
+        A.M[mi(A.rows, li, t)] = li == 0 ? A.row0[C] : current(A, t, li, C, A.T[li * A.ld + C]);
 }
 
 // ---------------------------------------------------------------------------
@@ -622,13 +624,13 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
             if (blockIdx.x == 0 && threadIdx.x == 0) ctl->r = rglob;
             return;
         }
-        a = A.M[R * BMAX + t];
+        a = A.M[mi(A.rows, R, t)];
     }
     if (a == 0.0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) ctl->status = LP_ZERO_PIVOT;
         return;
     }
-    const double f0 = A.M[t];            // row 0's multiplier (its current value at C)
+    const double f0 = A.M[mi(A.rows, 0, t)];   // row 0's multiplier (its current value at C)
     const long long j = blockIdx.x * (long long)PROW_THREADS + threadIdx.x;
     double v = INFINITY;
     if (j < A.ld) {
@@ -646,7 +648,7 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
         const long long stride = (long long)gridDim.x * blockDim.x;
         for (long long li = 1 + blockIdx.x * (long long)blockDim.x + threadIdx.x; li < A.rows;
              li += stride)
-            A.col0[li] = upd(li, R, A.M[li * BMAX + t], p0, A.col0[li]);
+            A.col0[li] = upd(li, R, A.M[mi(A.rows, li, t)], p0, A.col0[li]);
     }
     // entering-column summary of this slice of the new row 0
     const bool cand = j >= 1 && j <= A.n;
@@ -790,7 +792,13 @@ __device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[
         const unsigned b = threadIdx.x + k * blockDim.x;
         if (b < G && l[k] <= thr) { mine = b; kmine = k; }
     }
-    const long long bsel = block_min_ll(mine, sl);
+    long long bsel;
+    if constexpr (NR == 1) {     // summary b is lane b: the lowest lane in the band
+        const u64 mask = __ballot(mine != NONE);
+        bsel = mask ? (long long)__builtin_ctzll(mask) : NONE;
+    } else {
+        bsel = block_min_ll(mine, sl);
+    }
     if (bsel == NONE) return NONE;
     if (mine == bsel) {
         s_sel[0] = q[kmine] <= thr ? i[kmine] : -1 - bsel;
@@ -813,6 +821,9 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
     __shared__ double sPc[BMAX];       // P[s][C] for the current entering column
     __shared__ double sMr[BMAX];       // M[R][s] for the current leaving row
     __shared__ long long s_sel[2];
+    __shared__ long long sRp[BMAX];    // previous group (lag): local pivot rows
+    __shared__ double sPcp[BMAX];      //   P'[s][C]
+    __shared__ double sMrp[BMAX];      //   M'[R][s]
     // dynamic LDS: this block's rows' multipliers, its columns' pivot-row
     // slices and its slices of row 0 / column 0 (own data never leaves LDS
     // for a re-read; it is also published for the other blocks and the sweep)
@@ -821,7 +832,10 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
     const unsigned G = gridDim.x, b = blockIdx.x;
     const int tid = threadIdx.x;
     const int nth = blockDim.x;
-    if (b == 0 && tid == 0) ctl->ndef[grp ^ 1] = 0;   // the other parity's sweep is complete
+    // this parity's previous sweep is complete (the host orders it); the
+    // other parity holds the previous group, whose sweep may still be running
+    const int np = A.lag ? (int)ctl->ndef[grp ^ 1] : 0;
+    if (b == 0 && tid == 0) ctl->ndef[grp] = 0;
     if (ld_sc1(&ctl->status) != LP_PIVOTED) return;
     u64 *grR = A.gran;                         // ratio summaries [G][8]
     u64 *grE = A.gran + GROUP_MAXBLOCKS * 8;   // row-0 summaries [G][8]
@@ -833,10 +847,17 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
     double *lP = lM + rpb * count;           // [count][cpb]
     double *l0 = lP + count * cpb;           // [cpb]  row 0 slice
     double *lc = l0 + cpb;                   // [rpb]  column 0 slice
+    double *lMp = lc + rpb;                  // [np][rpb] previous group's multipliers (lag)
+    double *lPp = lMp + rpb * np;            // [np][cpb] previous group's pivot-row slices
     const long long li = lr0 + tid;          // this lane's own row
     const bool own = li < lr1;
     for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = A.row0[j];
     if (own) lc[tid] = A.col0[li];
+    for (int s = 0; s < np; ++s) {
+        if (own) lMp[s * rpb + tid] = A.Mp[mi(A.rows, li, s)];
+        for (long long j = jc0 + tid; j < jc1; j += nth) lPp[s * cpb + (j - jc0)] = A.Pp[s * A.ld + j];
+    }
+    if (tid < np) sRp[tid] = A.dRp[tid];
     const long long cap = ctl->cap;
     const int mode = ctl->mode;
     // counters live in registers for the launch (block 0 publishes them)
@@ -947,31 +968,38 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         //      load is issued before the cross-block loads (one round trip).
         double a = own ? A.T[li * A.ld + C] : 0.0;
         if (tid < t) sPc[tid] = ld_sc1(&A.P[tid * A.ld + C]);
+        if (tid < np) sPcp[tid] = A.Pp[tid * A.ld + C];
         if (tid == 0) {
             if (b == 0) st_sc1(&ctl->c, C - 1);
-            if (C >= jc0 && C < jc1) st_sc1(&A.M[t], l0[C - jc0]);   // row 0's multiplier
+            if (C >= jc0 && C < jc1) st_sc1(&A.M[mi(A.rows, 0, t)], l0[C - jc0]);   // row 0's multiplier
         }
         __syncthreads();
         stamp(A, t, 3);
-        for (int s0 = 0; s0 < t; s0 += CH) {
-            long long rr[CH];
-            double pc[CH], mm[CH];
+        // deferred pivots on the own row's element of column C: the previous
+        // group's (lag), then this group's 0..t-1, CH at a time
+        auto chain_col = [&](int nt, const long long *sr, const double *spc, const double *lm) {
+            for (int s0 = 0; s0 < nt; s0 += CH) {
+                long long rr[CH];
+                double pc[CH], mm[CH];
 #pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int s = min(s0 + u, count - 1);
-                rr[u] = sR[s];
-                pc[u] = sPc[s];
-                mm[u] = lM[s * rpb + min((long long)tid, rpb - 1)];
+                for (int u = 0; u < CH; ++u) {
+                    const int s = min(s0 + u, nt - 1);
+                    rr[u] = sr[s];
+                    pc[u] = spc[s];
+                    mm[u] = lm[s * rpb + min((long long)tid, rpb - 1)];
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (s0 + u < nt) a = upd(li, rr[u], mm[u], pc[u], a);
             }
-#pragma unroll
-            for (int u = 0; u < CH; ++u)
-                if (s0 + u < t) a = upd(li, rr[u], mm[u], pc[u], a);
-        }
+        };
+        chain_col(np, sRp, sPcp, lMp);
+        chain_col(t, sR, sPc, lM);
         double qown = 0.0;
         bool okown = false;
         if (own) {
             lM[t * rpb + tid] = a;
-            st_sc1(&A.M[li * BMAX + t], a);
+            st_sc1(&A.M[mi(A.rows, li, t)], a);
             qown = row_ratio(a, lc[tid], A.tol, okown);
         }
         const double lb = block_min(own && okown ? qown : INFINITY, sd);
@@ -1032,7 +1060,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
             long long mine = NONE;
             for (long long lj = r0 + tid; lj < r1; lj += nth) {
                 bool ok;
-                const double q = row_ratio(ld_sc1(&A.M[lj * BMAX + t]), ld_sc1(&A.col0[lj]), A.tol, ok);
+                const double q = row_ratio(ld_sc1(&A.M[mi(A.rows, lj, t)]), ld_sc1(&A.col0[lj]), A.tol, ok);
                 if (ok && q <= thr) { mine = lj; break; }
             }
             R = block_min_ll(mine, sl);
@@ -1046,36 +1074,46 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
             const long long j = jc0 + tid + k * nth;
             xv[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
         }
-        if (tid <= t) sMr[tid] = ld_sc1(&A.M[R * BMAX + tid]);
+        if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, R, tid)]);
+        if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, R, tid)];
         if (tid == 0) sR[t] = R;
-        const double f0 = ld_sc1(&A.M[t]);
+        const double f0 = ld_sc1(&A.M[mi(A.rows, 0, t)]);
         __syncthreads();
         stamp(A, t, 8);
         const double av = sMr[t];
         // deferred pivots 0..t-1 of the group on the own columns, CH at a time
-        auto chain = [&](double (&x)[IPL], long long kbase) {
-            for (int s0 = 0; s0 < t; s0 += CH) {
+        auto chain1 = [&](double (&x)[IPL], long long kbase, int nt, const long long *sr,
+                          const double *smr, const double *lp) {
+            for (int s0 = 0; s0 < nt; s0 += CH) {
                 long long rr[CH];
                 double mr[CH], pv[CH][IPL];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
-                    const int s = min(s0 + u, count - 1);
-                    rr[u] = sR[s];
-                    mr[u] = sMr[s];
+                    const int s = min(s0 + u, nt - 1);
+                    rr[u] = sr[s];
+                    mr[u] = smr[s];
 #pragma unroll
                     for (int k = 0; k < IPL; ++k)
-                        pv[u][k] = lP[s * cpb + min(kbase + k * nth, cpb - 1)];
+                        pv[u][k] = lp[s * cpb + min(kbase + k * nth, cpb - 1)];
                 }
 #pragma unroll
                 for (int u = 0; u < CH; ++u)
-                    if (s0 + u < t) {
+                    if (s0 + u < nt) {
+                        if (R == rr[u]) {          // row R was pivot row s
 #pragma unroll
-                        for (int k = 0; k < IPL; ++k) x[k] = upd(R, rr[u], mr[u], pv[u][k], x[k]);
+                            for (int k = 0; k < IPL; ++k) x[k] = pv[u][k];
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < IPL; ++k) x[k] = fma(-mr[u], pv[u][k], x[k]);
+                        }
                     }
             }
         };
+        auto chain = [&](double (&x)[IPL], long long kbase) {
+            chain1(x, kbase, np, sRp, sMrp, lPp);
+            chain1(x, kbase, t, sR, sMr, lP);
+        };
         double vmin = INFINITY, v0 = 0.0;
-        long long fneg = NONE;
         auto finish_col = [&](long long j, double x) {
             const long long k = j - jc0;
             const double p = (j == C) ? 1.0 : x / av;
@@ -1085,10 +1123,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
             l0[k] = v;
             st_sc1(&A.row0[j], v);
             if (j == 0) v0 = v;
-            if (j >= 1 && j <= A.n) {
-                vmin = fmin(vmin, v);
-                if (v < -A.tol.cost && j < fneg) fneg = j;
-            }
+            if (j >= 1 && j <= A.n) vmin = fmin(vmin, v);
         };
         chain(xv, tid);
 #pragma unroll
@@ -1112,23 +1147,32 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         }
         __syncthreads();
         stamp(A, t, 9);
-        // row-0 summary of own columns
+        // row-0 summary of own columns: columns j = jc0 + lane + 64k, so the
+        // first column with a property is the lowest lane of the first k
+        // whose ballot is non-empty
         const double el = block_min(vmin, sd);
-        const long long efn = block_min_ll(fneg, sl);
+        long long efn = NONE;
+        for (long long j0 = jc0; j0 < jc1 && efn == NONE; j0 += nth) {
+            const long long j = j0 + tid;
+            const bool ok = j < jc1 && j >= 1 && j <= A.n && l0[j - jc0] < -A.tol.cost;
+            const u64 mask = __ballot(ok);
+            if (mask) efn = j0 + __builtin_ctzll(mask);
+        }
         long long ei = NONE;
         double eq = 0.0;
         if (el < INFINITY) {
             const double ethr = tie_band(el, A.tol.cost_tie);
-            long long mine = NONE;
-            double vmine = 0.0;
-            for (long long j = jc0 + tid; j < jc1; j += nth) {
-                const double v = l0[j - jc0];
-                if (j >= 1 && j <= A.n && v <= ethr) { mine = j; vmine = v; break; }
+            for (long long j0 = jc0; j0 < jc1; j0 += nth) {
+                const long long j = j0 + tid;
+                const double v = j < jc1 ? l0[j - jc0] : INFINITY;
+                const u64 mask = __ballot(j >= 1 && j <= A.n && v <= ethr);
+                if (mask) {
+                    const int f = __builtin_ctzll(mask);
+                    ei = j0 + f;
+                    eq = mk_d(__builtin_amdgcn_readlane(lo32(v), f), __builtin_amdgcn_readlane(hi32(v), f));
+                    break;
+                }
             }
-            ei = block_min_ll(mine, sl);
-            const u64 mask = __ballot(mine == ei);
-            const int f = __builtin_ctzll(mask);
-            eq = mk_d(__builtin_amdgcn_readlane(lo32(vmine), f), __builtin_amdgcn_readlane(hi32(vmine), f));
         }
         stamp(A, t, 10);
         if (b == 0 && tid == 0) {     // column 0 is in block 0's slice: v0 = new row0[0]
@@ -1198,89 +1242,103 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
 }
 
 // ---------------------------------------------------------------------------
-// K3: the sweep.  T <- T with the group's deferred pivots 0..ndef-1 applied.
-//   Tile = 128 columns (one wave: 64 lanes x 16 B) x SWEEP_ROWS rows; the
-//   four waves of a block take interleaved rows.  Each lane keeps its slice
-//   of the ND deferred pivot rows in registers; a row's ND multipliers are one
-//   scalar load (M is row-major), so every row-level test is a scalar branch
-//   and the inner loop is just two FMAs per deferred pivot.  Tiles that hold
-//   one of the (at most ND) pivot rows take the general path.  Each element
-//   is loaded once and stored once.
+// K3: the sweep.  T_out <- T with the group's deferred pivots 0..ndef-1
+//   applied (T_out == T: in place).  Tile = 128 columns x SWEEP_ROWS rows per
+//   block of SWEEP_WAVES waves; a lane owns 2 columns (16-byte accesses) of SWEEP_RW
+//   rows, all loaded up front and held in registers while the pivots are
+//   applied in order: per pivot one LDS read of the lane's pivot-row values
+//   (the block's slice of P is staged in LDS once) and one wide scalar load
+//   of the SWEEP_RW rows' multipliers (M is pivot-major), then 2 FMAs per
+//   row.  Registers do not grow with the number of pivots, so any group size
+//   streams at the same occupancy.  Tiles holding one of the (at most ndef)
+//   pivot rows take a select per row.  Each element is loaded and stored once.
 // ---------------------------------------------------------------------------
 
-template <int ND>
-__global__ void __launch_bounds__(256)
-k_sweep(double *__restrict__ T, const double *__restrict__ P, const double *__restrict__ M,
-        const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld,
-        long long rows, int grp)
+template <int SWEEP_WAVES, int SWEEP_RW, int SWEEP_NG>
+__global__ void __launch_bounds__(64 * SWEEP_WAVES)
+k_sweep(const double *T, double *Tout, const double *__restrict__ P,
+        const double *__restrict__ M, const long long *__restrict__ dR,
+        const Ctl *__restrict__ ctl, long long ld, long long rows, int grp)
 {
-    const int nd = (int)ctl->ndef[grp];     // <= ND
+    constexpr int SWEEP_ROWS = SWEEP_WAVES * SWEEP_RW * SWEEP_NG;
+    __shared__ double2 sp[BMAX][64];          // the block's 128-column slice of P
+    __shared__ long long sr[BMAX];            // pivot rows
+    const int nd = (int)ctl->ndef[grp];
     if (nd == 0) return;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long j0 = (long long)blockIdx.x * 128 + lane * 2;
-    const long long r0 = (long long)blockIdx.y * SWEEP_ROWS;
-    const long long rend = min(r0 + SWEEP_ROWS, rows);
     const bool active = j0 < ld;
-    // pivots s >= nd are padded as f = +0, P = +0: fma(-0, +0, y) == y exactly
-    double2 p[ND];
-    bool pivrow_here = false;
+    for (int s = wave; s < nd; s += SWEEP_WAVES)
+        sp[s][lane] = active ? *reinterpret_cast<const double2 *>(P + s * ld + j0)
+                             : make_double2(0.0, 0.0);
+    if (threadIdx.x < nd) sr[threadIdx.x] = dR[threadIdx.x];
+    const long long base = (long long)blockIdx.y * SWEEP_ROWS;
+    // row group g of this wave: rows [rb(g), rb(g) + SWEEP_RW)
+    auto rb_of = [&](int g) { return base + (long long)(g * SWEEP_WAVES + wave) * SWEEP_RW; };
+    // rows past the end re-load the last row (in bounds) and are not stored
+    auto load = [&](double2 (&x)[SWEEP_RW], long long rb) {
+        if (!active || rb >= rows) return;
 #pragma unroll
-    for (int s = 0; s < ND; ++s) {
-        p[s] = make_double2(0.0, 0.0);
-        if (s < nd) {
-            if (active) p[s] = *reinterpret_cast<const double2 *>(P + s * ld + j0);
-            const long long R = dR[s];
-            pivrow_here |= (R >= r0 && R < rend);
+        for (int k = 0; k < SWEEP_RW; ++k)
+            x[k] = *reinterpret_cast<const double2 *>(T + min(rb + k, rows - 1) * ld + j0);
+    };
+    auto apply = [&](double2 (&x)[SWEEP_RW], long long rb) {
+        if (!active || rb >= rows) return;
+        const long long nr = min((long long)SWEEP_RW, rows - rb);
+        bool pivrow_here = false;
+        for (int s = 0; s < nd; ++s) {
+            const long long R = sr[s];
+            pivrow_here |= (R >= rb && R < rb + nr);
         }
-    }
-    if (!active) return;
-    double *base = T + j0;
-    for (long long i = r0 + wave; i < rend; i += 4 * SWEEP_UNROLL) {
-        // rows past the tile end re-load the last row (in bounds) and are not stored
-        double2 x[SWEEP_UNROLL];
+        const double *mt = M + rb;             // M[s * rows + rb + k]
+        if (!pivrow_here) {
+#pragma unroll 2
+            for (int s = 0; s < nd; ++s) {
+                const double2 pv = sp[s][lane];
+                const double *f = mt + s * rows;
+                double fk[SWEEP_RW];
 #pragma unroll
-        for (int u = 0; u < SWEEP_UNROLL; ++u) {
-            const long long ii = min(i + 4 * u, rend - 1);
-            x[u] = *reinterpret_cast<const double2 *>(base + ii * ld);
-        }
+                for (int k = 0; k < SWEEP_RW; ++k) fk[k] = f[k];
 #pragma unroll
-        for (int u = 0; u < SWEEP_UNROLL; ++u) {
-            const long long ii = i + 4 * u;
-            if (ii >= rend) break;
-            double fr[ND];                      // one wide scalar load per row
-            const double *f = M + ii * BMAX;
-#pragma unroll
-            for (int s = 0; s < ND; ++s) {
-                const double v = f[s];
-                fr[s] = s < nd ? v : 0.0;
-            }
-            double2 y = x[u];
-            if (!pivrow_here) {
-#pragma unroll
-                for (int s = 0; s < ND; ++s) {
-                    y.x = fma(-fr[s], p[s].x, y.x);
-                    y.y = fma(-fr[s], p[s].y, y.y);
+                for (int k = 0; k < SWEEP_RW; ++k) {
+                    x[k].x = fma(-fk[k], pv.x, x[k].x);
+                    x[k].y = fma(-fk[k], pv.y, x[k].y);
                 }
-            } else {
+            }
+        } else {
+            for (int s = 0; s < nd; ++s) {
+                const double2 pv = sp[s][lane];
+                const double *f = mt + s * rows;
+                const long long kr = sr[s] - rb;   // this pivot's row in the group, if any
 #pragma unroll
-                for (int s = 0; s < ND; ++s) {
-                    if (s < nd) {
-                        if (ii == dR[s]) {
-                            y = p[s];
-                        } else {
-                            y.x = fma(-fr[s], p[s].x, y.x);
-                            y.y = fma(-fr[s], p[s].y, y.y);
-                        }
+                for (int k = 0; k < SWEEP_RW; ++k) {
+                    const double fk = f[k];
+                    if (k == kr) {
+                        x[k] = pv;
+                    } else {
+                        x[k].x = fma(-fk, pv.x, x[k].x);
+                        x[k].y = fma(-fk, pv.y, x[k].y);
                     }
                 }
             }
-            *reinterpret_cast<double2 *>(base + ii * ld) = y;
         }
+#pragma unroll
+        for (int k = 0; k < SWEEP_RW; ++k)
+            if (k < nr) *reinterpret_cast<double2 *>(Tout + (rb + k) * ld + j0) = x[k];
+    };
+    // software pipeline over the wave's row groups: group g+1 is in flight
+    // while group g is updated
+    double2 x[2][SWEEP_RW];
+    load(x[0], rb_of(0));
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < SWEEP_NG; ++g) {
+        if (g + 1 < SWEEP_NG) load(x[(g + 1) & 1], rb_of(g + 1));
+        apply(x[g & 1], rb_of(g));
     }
 }
 
-// after a straddle: the group was swept up to the straddling pivot; continue
 __global__ void k_resume(Ctl *ctl)
 {
     ctl->status = LP_PIVOTED;
@@ -1371,35 +1429,39 @@ hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, i
     return hipGetLastError();
 }
 
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max)
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out)
 {
-    const dim3 grid((unsigned)((A.ld + 127) / 128),
-                    (unsigned)((A.rows + SWEEP_ROWS - 1) / SWEEP_ROWS));
-#define SWEEP_CASE(N)                                                                        \
-    case N:                                                                                  \
-        hipLaunchKernelGGL(k_sweep<N>, grid, dim3(256), 0, s, A.T, A.P, A.M, A.dR, A.ctl,   \
-                           A.ld, A.rows, grp);                                               \
-        break;
-    switch (bound_of(nd_max < 1 ? 1 : nd_max)) {
-        SWEEP_CASE(1)
-        SWEEP_CASE(2)
-        SWEEP_CASE(4)
-        SWEEP_CASE(8)
-        SWEEP_CASE(16)
-        default:
-        SWEEP_CASE(32)
+    (void)nd_max;
+    static int variant = -1;
+    if (variant < 0) {
+        variant = 0;
+        if (const char *v = getenv("LPGPU_SWEEP")) variant = atoi(v);
     }
-#undef SWEEP_CASE
+#define SWEEP_LAUNCH(W, RW, NG)                                                              \
+    hipLaunchKernelGGL((k_sweep<W, RW, NG>),                                                 \
+                       dim3((unsigned)((A.ld + 127) / 128),                                  \
+                            (unsigned)((A.rows + W * RW * NG - 1) / (W * RW * NG))),         \
+                       dim3(64 * W), 0, s, A.T, T_out, A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp)
+    switch (variant) {
+    case 1: SWEEP_LAUNCH(4, 8, 2); break;
+    case 2: SWEEP_LAUNCH(8, 8, 2); break;
+    case 3: SWEEP_LAUNCH(8, 8, 4); break;
+    case 4: SWEEP_LAUNCH(4, 16, 1); break;
+    case 5: SWEEP_LAUNCH(4, 8, 4); break;
+    case 6: SWEEP_LAUNCH(2, 8, 4); break;
+    default: SWEEP_LAUNCH(8, 8, 1); break;
+    }
+#undef SWEEP_LAUNCH
     return hipGetLastError();
 }
 
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq)
+                        unsigned seq, int bmax)
 {
-    if (count < 1 || count > BMAX) return hipErrorInvalidValue;
-    const long long g = group_blocks(A.rc, A.ld, count);
+    if (count < 1 || count > bmax || bmax > BMAX) return hipErrorInvalidValue;
+    const long long g = group_blocks(A.rc, A.ld, bmax, A.lag);
     if (g == 0) return hipErrorInvalidValue;
-    const size_t lds = (size_t)group_lds(A.rc, A.ld, g, count);
+    const size_t lds = (size_t)group_lds(A.rc, A.ld, g, bmax, A.lag);
     const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
     if (nr <= 1)
         hipLaunchKernelGGL(k_group<1>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp,

@@ -41,11 +41,18 @@ struct lp_handle {
     double *T = nullptr, *P = nullptr, *M = nullptr, *row0 = nullptr, *col0 = nullptr;
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
-    int block = 16;                 // pivots deferred into one sweep (1..BMAX)
+    int block = 32;                 // pivots deferred into one sweep (1..BMAX)
     bool persistent = true;         // single device: one k_group launch per group
     long long *stamps = nullptr;    // diagnostic phase clocks (LPGPU_STAMPS=1)
     unsigned long long *gran = nullptr;  // k_group summaries (tagged granules)
     unsigned gseq = 0;              // k_group launches so far (tags their summaries)
+    // pipelined groups (single device): group g's sweep (out of place, T -> T2)
+    // runs on its own CUs while group g+1 is selected on the others
+    bool pipeline = false;          // LPGPU_PIPELINE=1: measured slower on cfg3 (memory contention)
+    double *T2 = nullptr;           // second tableau buffer
+    hipStream_t ssel = nullptr, ssw = nullptr;   // CU-partitioned streams
+    int sel_cus = 0;                // CUs of the selection stream
+    std::vector<hipEvent_t> pev;    // ordering events, reused per batch
     bool eager_ok = false;          // row0/col0 mirror the stored tableau
     Ctl *ctl = nullptr;
     Ctl *hctl = nullptr;            // pinned mirror
@@ -195,6 +202,30 @@ static Args args_of(const lp_handle *h)
     A.tol = h->tol;
     A.stamps = h->stamps;
     A.gran = h->gran;
+    A.Pp = nullptr;
+    A.Mp = nullptr;
+    A.dRp = nullptr;
+    A.lag = 0;
+    A.pad2 = 0;
+    return A;
+}
+
+// arguments of a pipelined group of parity par reading tableau buffer T
+// (lag: the previous group, parity par ^ 1, is not yet swept into T)
+static Args args_par(const lp_handle *h, int par, double *T, int lag)
+{
+    Args A = args_of(h);
+    const size_t pstride = (size_t)lpk::BMAX * h->ld;
+    const size_t mstride = (size_t)lpk::BMAX * h->rows + lpk::M_PAD;
+    A.T = T;
+    A.P = h->P + par * pstride;
+    A.M = h->M + par * mstride;
+    A.dR = h->dR + par * lpk::BMAX;
+    A.dC = h->dC + par * lpk::BMAX;
+    A.Pp = h->P + (par ^ 1) * pstride;
+    A.Mp = h->M + (par ^ 1) * mstride;
+    A.dRp = h->dR + (par ^ 1) * lpk::BMAX;
+    A.lag = lag;
     return A;
 }
 
@@ -232,6 +263,8 @@ static int alloc_handle(lp_handle *h)
 {
     if (const char *sel = std::getenv("LPGPU_SELECT"))
         h->persistent = std::strcmp(sel, "kernels") != 0;
+    if (const char *pl = std::getenv("LPGPU_PIPELINE")) h->pipeline = pl[0] == '1';
+    if (const char *sc = std::getenv("LPGPU_SEL_CUS")) h->sel_cus = std::atoi(sc);
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
             HCHK(h, hipMalloc(&h->stamps, lpk::BMAX * 16 * sizeof(long long)));
@@ -242,10 +275,12 @@ static int alloc_handle(lp_handle *h)
     const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
     HCHK(h, hipMalloc(&h->T, tbytes));
     HCHK(h, hipMemsetAsync(h->T, 0, tbytes, h->s));
-    HCHK(h, hipMalloc(&h->P, (size_t)lpk::BMAX * h->ld * sizeof(double)));
-    HCHK(h, hipMemsetAsync(h->P, 0, (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
-    HCHK(h, hipMalloc(&h->M, (size_t)lpk::BMAX * h->rows * sizeof(double)));
-    HCHK(h, hipMemsetAsync(h->M, 0, (size_t)lpk::BMAX * h->rows * sizeof(double), h->s));
+    // two sets of group data (P, M, dR, dC) by group parity
+    HCHK(h, hipMalloc(&h->P, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double)));
+    HCHK(h, hipMemsetAsync(h->P, 0, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
+    const size_t mbytes = 2 * ((size_t)lpk::BMAX * h->rows + lpk::M_PAD) * sizeof(double);
+    HCHK(h, hipMalloc(&h->M, mbytes));
+    HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
     const size_t gbytes = 2 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
     HCHK(h, hipMalloc(&h->gran, gbytes));
     HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
@@ -253,8 +288,8 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMemsetAsync(h->row0, 0, (size_t)h->ld * sizeof(double), h->s));
     HCHK(h, hipMalloc(&h->col0, (size_t)h->rows * sizeof(double)));
     HCHK(h, hipMemsetAsync(h->col0, 0, (size_t)h->rows * sizeof(double), h->s));
-    HCHK(h, hipMalloc(&h->dR, (size_t)lpk::BMAX * sizeof(long long)));
-    HCHK(h, hipMalloc(&h->dC, (size_t)lpk::BMAX * sizeof(long long)));
+    HCHK(h, hipMalloc(&h->dR, 2 * (size_t)lpk::BMAX * sizeof(long long)));
+    HCHK(h, hipMalloc(&h->dC, 2 * (size_t)lpk::BMAX * sizeof(long long)));
     HCHK(h, hipMalloc(&h->erec, (size_t)std::max(lpk::GROUP_MAXBLOCKS, lpk::prow_blocks(h->ld)) *
                                      sizeof(lpk::ERec)));
     h->eager_ok = true;   // all zero
@@ -405,6 +440,12 @@ extern "C" int lp_destroy(lp_handle *h)
     (void)hipSetDevice(h->dev);
     if (h->s) (void)hipStreamSynchronize(h->s);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->ssel) (void)hipStreamSynchronize(h->ssel);
+    if (h->ssw) (void)hipStreamSynchronize(h->ssw);
+    for (hipEvent_t e : h->pev) (void)hipEventDestroy(e);
+    if (h->ssel) (void)hipStreamDestroy(h->ssel);
+    if (h->ssw) (void)hipStreamDestroy(h->ssw);
+    if (h->T2) (void)hipFree(h->T2);
     if (h->T) (void)hipFree(h->T);
     if (h->P) (void)hipFree(h->P);
     if (h->M) (void)hipFree(h->M);
@@ -541,10 +582,13 @@ static int ensure_log(lp_handle *h, int64_t need)
     return LP_PIVOTED;
 }
 
-static int launch_sweep_timed(lp_handle *h, const Args &A, int grp)
+static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, hipStream_t st = nullptr,
+                              double *T_out = nullptr)
 {
+    if (!st) st = h->s;
+    if (!T_out) T_out = A.T;
     if (!h->prof) {
-        HCHK(h, lpk::launch_sweep(h->s, A, grp, h->block));
+        HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out));
         return LP_PIVOTED;
     }
     if (h->evused + 2 > h->ev.size()) {
@@ -554,9 +598,9 @@ static int launch_sweep_timed(lp_handle *h, const Args &A, int grp)
         h->ev.push_back(a);
         h->ev.push_back(b);
     }
-    HCHK(h, hipEventRecord(h->ev[h->evused], h->s));
-    HCHK(h, lpk::launch_sweep(h->s, A, grp, h->block));
-    HCHK(h, hipEventRecord(h->ev[h->evused + 1], h->s));
+    HCHK(h, hipEventRecord(h->ev[h->evused], st));
+    HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out));
+    HCHK(h, hipEventRecord(h->ev[h->evused + 1], st));
     h->evused += 2;
     return LP_PIVOTED;
 }
@@ -665,6 +709,98 @@ static int begin_call(const Members &M, const std::vector<Args> &A, int mode, in
     return LP_PIVOTED;
 }
 
+// ---------------------------------------------------------------------------
+// pipelined groups (single device)
+// ---------------------------------------------------------------------------
+
+// second tableau buffer and two CU-partitioned streams: the latency-bound
+// selection keeps sel_cus CUs to itself, the bandwidth-bound sweep streams on
+// the rest, so neither waits behind the other's waves
+static int ensure_pipeline(lp_handle *h, long long g)
+{
+    if (h->T2 && h->ssel && h->ssw) return LP_PIVOTED;
+    HCHK(h, hipSetDevice(h->dev));
+    if (!h->T2) {
+        const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
+        HCHK(h, hipMalloc(&h->T2, tbytes));
+        HCHK(h, hipMemsetAsync(h->T2, 0, tbytes, h->s));   // padding columns stay 0
+    }
+    int ncu = 0;
+    HCHK(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev));
+    int nsel = h->sel_cus > 0 ? h->sel_cus : (int)std::min<long long>(g, ncu / 4);
+    nsel = std::max(1, std::min(nsel, ncu / 2));
+    std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mw((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) (c < nsel ? ms : mw)[c / 32] |= 1u << (c % 32);
+    HCHK(h, hipExtStreamCreateWithCUMask(&h->ssel, (uint32_t)ms.size(), ms.data()));
+    HCHK(h, hipExtStreamCreateWithCUMask(&h->ssw, (uint32_t)mw.size(), mw.data()));
+    h->sel_cus = nsel;
+    return LP_PIVOTED;
+}
+
+static int pev_at(lp_handle *h, size_t k, hipEvent_t *e)
+{
+    while (h->pev.size() <= k) {
+        hipEvent_t x;
+        HCHK(h, hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        h->pev.push_back(x);
+    }
+    *e = h->pev[k];
+    return LP_PIVOTED;
+}
+
+// b pivots as groups of B: selection of group g (stream ssel) overlaps the
+// sweep of group g-1 (stream ssw).  Group g reads S_{g-1} (the tableau with
+// groups < g-1 applied) and applies group g-1's pivots on the fly; the sweep
+// of group g writes S_{g+1} into the other buffer.  Returns the number of
+// groups enqueued; the caller syncs and settles the buffers (settle_buffers).
+static int enqueue_pipelined(lp_handle *h, int64_t b, bool &chained, int *ngroups)
+{
+    const int B = h->block;
+    const long long g = lpk::group_blocks(h->rc, h->ld, B, 1);
+    CALL(ensure_pipeline(h, g));
+    double *buf[2] = {h->T, h->T2};
+    size_t ne = 0;
+    hipEvent_t e0, esel, last_sel = nullptr;
+    std::vector<hipEvent_t> esw;
+    CALL(pev_at(h, ne++, &e0));
+    HCHK(h, hipEventRecord(e0, h->s));
+    HCHK(h, hipStreamWaitEvent(h->ssel, e0, 0));
+    HCHK(h, hipStreamWaitEvent(h->ssw, e0, 0));
+    int gi = 0;
+    for (int64_t k = 0; k < b; k += B, ++gi) {
+        const int cnt = (int)std::min<int64_t>(B, b - k);
+        const int par = gi & 1;
+        Args A = args_par(h, par, buf[gi == 0 ? 0 : (gi - 1) & 1], gi > 0 ? 1 : 0);
+        if (gi >= 2) HCHK(h, hipStreamWaitEvent(h->ssel, esw[gi - 2], 0));
+        h->gseq = h->gseq % ((1u << 26) - 1) + 1;
+        HCHK(h, lpk::launch_group(h->ssel, A, par, cnt, chained ? 1 : 0, h->gseq, B));
+        CALL(pev_at(h, ne++, &esel));
+        HCHK(h, hipEventRecord(esel, h->ssel));
+        last_sel = esel;
+        HCHK(h, hipStreamWaitEvent(h->ssw, esel, 0));
+        Args S = args_par(h, par, buf[gi & 1], 0);
+        CALL(launch_sweep_timed(h, S, par, h->ssw, buf[(gi + 1) & 1]));
+        hipEvent_t e;
+        CALL(pev_at(h, ne++, &e));
+        HCHK(h, hipEventRecord(e, h->ssw));
+        esw.push_back(e);
+        chained = true;
+    }
+    if (last_sel) HCHK(h, hipStreamWaitEvent(h->s, last_sel, 0));
+    if (!esw.empty()) HCHK(h, hipStreamWaitEvent(h->s, esw.back(), 0));
+    *ngroups = gi;
+    return LP_PIVOTED;
+}
+
+// after the sync: groups that performed pivots were swept in order, so the
+// current tableau is S_k in buffer k & 1 (k = those groups)
+static void settle_buffers(lp_handle *h, int64_t pivots, int ngroups)
+{
+    const int B = h->block;
+    const int64_t k = std::min<int64_t>(ngroups, (pivots + B - 1) / B);
+    if (k & 1) std::swap(h->T, h->T2);
+}
+
 // Runs pivots until the device reports a status other than LP_PIVOTED or
 // `limit` pivots have been enqueued (limit < 0: unlimited).  Pivots are
 // enqueued in groups of `block` followed by one sweep; the host knows each
@@ -687,12 +823,18 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         if (limit >= 0) b = std::min(b, limit - done);
         for (lp_handle *x : M) CALL(ensure_log(x, done + b + 1));
         A = args_all(M);
-        if (!h->comm && h->persistent && lpk::group_blocks(h->rc, h->ld, B) > 0) {
-            // one persistent selection launch + one sweep per group
+        const bool pipelined = !h->comm && h->persistent && h->pipeline &&
+                               lpk::group_blocks(h->rc, h->ld, B, 1) > 0;
+        int ngroups = 0;
+        const int64_t before = done;
+        if (pipelined) {
+            CALL(enqueue_pipelined(h, b, chained, &ngroups));
+        } else if (!h->comm && h->persistent && lpk::group_blocks(h->rc, h->ld, B, 0) > 0) {
+            // one persistent selection launch + one in-place sweep per group
             for (int64_t k = 0; k < b; k += B) {
                 const int cnt = (int)std::min<int64_t>(B, b - k);
                 h->gseq = h->gseq % ((1u << 26) - 1) + 1;
-                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0, h->gseq));
+                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0, h->gseq, B));
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
                 chained = true;
@@ -710,7 +852,8 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             }
         }
         CALL(sync_ctl(M));
-        if (h->hctl->bar_timeout) return fail(h, LP_DEVICE_ERROR, "k_group grid barrier timed out");
+        if (pipelined) settle_buffers(h, h->hctl->npiv - before, ngroups);
+        if (h->hctl->bar_timeout) return fail(h, LP_DEVICE_ERROR, "k_group summary exchange timed out");
         if (h->hctl->status == lpk::ST_STRADDLE) {
             // rare near-tie across ranks: the pivots before it are swept and
             // ctl->c holds its entering column; redo it with two exchanges

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "liblpgpu.so")
+# LPGPU_LIB selects another build of the same library (A/B timing of variants)
+LIB_PATH = os.environ.get("LPGPU_LIB") or os.path.join(HERE, "_lib", "liblpgpu.so")
 
 # lp_status
 PIVOTED, OPTIMAL, UNBOUNDED = 0, 1, 2

@@ -41,6 +41,40 @@ for step in "$@"; do
         prof)
             export TMPDIR=/tmp
             run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$PWD/bench.py" --steps 200 --no-cpu-baseline ;;
+        pipe)
+            LPGPU_PIPELINE=0 run bench_nopipe 300 python bench.py --no-cpu-baseline
+            for C in 32 64 96; do
+                LPGPU_SEL_CUS=$C run bench_sel$C 300 python bench.py --no-cpu-baseline
+            done
+            run bench_pipe_b32 300 python bench.py --no-cpu-baseline --block 32
+            run bench_pipe_b8 300 python bench.py --no-cpu-baseline --block 8 ;;
+        sweepvw)
+            for B in 16 32; do
+                LPGPU_PIPELINE=0 run bench_np_b$B 300 python bench.py --no-cpu-baseline --block $B
+                run bench_p_b$B 300 python bench.py --no-cpu-baseline --block $B
+            done ;;
+        sweepvar)
+            for V in 0 1 2 3 4 5 6; do
+                for B in 16 32; do
+                    LPGPU_PIPELINE=0 LPGPU_SWEEP=$V run bench_v${V}_b$B 300 python bench.py --no-cpu-baseline --block $B --steps 512
+                done
+            done ;;
+        ab)
+            # A/B of library variants built by `make -C linear-program-solver_amd/csrc variant`
+            for rep in 1 2; do
+                for V in ${AB_VARIANTS:-all}; do
+                    L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/$V.so
+                    LPGPU_LIB=$L run stamps_${V}_$rep 300 python scripts/diag_stamps.py
+                    LPGPU_LIB=$L LPGPU_PIPELINE=0 run bench_${V}_$rep 300 python bench.py --no-cpu-baseline --steps 512 --block ${AB_BLOCK:-16}
+                done
+            done ;;
+        modes)
+            for rep in 1 2; do
+                for B in 16 32; do
+                    LPGPU_PIPELINE=0 run bench_np_b${B}_$rep 300 python bench.py --no-cpu-baseline --steps 1024 --block $B
+                    LPGPU_PIPELINE=1 run bench_p_b${B}_$rep 300 python bench.py --no-cpu-baseline --steps 1024 --block $B
+                done
+            done ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
         pmc)

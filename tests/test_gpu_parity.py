@@ -45,11 +45,14 @@ def _initial_basis(T):
     return bc
 
 
-@pytest.fixture(params=["persistent", "kernels"])
+@pytest.fixture(params=["pipelined", "persistent", "kernels"])
 def select_mode(request, monkeypatch):
-    """single-device selection path: one persistent k_group launch per group,
-    or the per-pivot k_ratio/k_prow launches (the sharded path's kernels)"""
-    monkeypatch.setenv("LPGPU_SELECT", request.param)
+    """single-device selection path: persistent k_group launches whose sweeps
+    run concurrently on their own CUs (default), the same with in-place sweeps
+    after each group, or the per-pivot k_ratio/k_prow launches (the sharded
+    path's kernels)"""
+    monkeypatch.setenv("LPGPU_SELECT", "kernels" if request.param == "kernels" else "persistent")
+    monkeypatch.setenv("LPGPU_PIPELINE", "1" if request.param == "pipelined" else "0")
     return request.param
 
 
