@@ -150,29 +150,42 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 // the launch's summaries so no stale granule can match
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
                         unsigned seq, int bmax);
-constexpr int GROUP_BLOCKS = 64;   // co-resident workgroups of k_group (<= CUs) ...
+#ifndef LPK_GROUP_BLOCKS
+#define LPK_GROUP_BLOCKS 64
+#endif
+#ifndef LPK_GROUP_ROWS
+#define LPK_GROUP_ROWS 64
+#endif
+constexpr int GROUP_BLOCKS = LPK_GROUP_BLOCKS;   // co-resident workgroups of k_group (<= CUs) ...
 constexpr int GROUP_MAXBLOCKS = 256;
-constexpr int GROUP_ROWS = 64;     // ... raised so a block owns at most this many rows
+constexpr int GROUP_ROWS = LPK_GROUP_ROWS;       // ... raised so a block owns at most this many rows
 constexpr int GROUP_THREADS = 64;  // one wave: block reductions stay in registers
 constexpr long long GROUP_LDS_MAX = 96 * 1024;
-// dynamic LDS of one k_group block (own multipliers, pivot-row slices, row 0
-// and column 0 slices; with a lagging previous group of up to `count` pivots
-// its multipliers and pivot-row slices too)
+// dynamic LDS of one k_group block: per own row / own column the pivots'
+// values at stride count + 1 (multipliers, pivot-row values; twice with a
+// lagging previous group of up to `count` pivots) + row 0 / column 0 slices
 __host__ __device__ inline long long group_lds(long long rc, long long ld, long long g, int count,
                                                int lag)
 {
     const long long rpb = (rc + g - 1) / g, cpb = (ld + g - 1) / g;
-    return ((rpb * count + count * cpb) * (lag ? 2 : 1) + cpb + rpb) * 8;
+    return ((rpb + cpb) * (count + 1) * (lag ? 2 : 1) + cpb + rpb + 8) * 8;   // + a chunk of slack
 }
-// workgroups of k_group for this shape, 0 if its LDS would not fit (the
-// per-pivot kernels are used instead)
+// workgroups of k_group for this shape, 0 if it does not fit (the per-pivot
+// kernels are used instead): a block owns at most GROUP_ROWS rows (one per
+// lane) and at most 4 columns per lane; a few extra blocks are taken when
+// that brings every lane down to 2 columns
 __host__ __device__ inline long long group_blocks(long long rc, long long ld, int count, int lag)
 {
     if (ld >= 0x7fffffffLL || rc >= 0x7fffffffLL) return 0;   // indices travel as 31 bits
     long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
     if (g < GROUP_BLOCKS) g = GROUP_BLOCKS;
+    const long long g2 = (ld + 2 * GROUP_THREADS - 1) / (2 * GROUP_THREADS);
+    const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
+    if (g2 > g && g2 <= g + g / 8) g = g2;
+    if (g4 > g) g = g4;
     while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX) g *= 2;
     if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
+    if ((ld + g - 1) / g > 4 * GROUP_THREADS) return 0;
     return group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX ? 0 : g;
 }
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);

@@ -777,61 +777,58 @@ __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[
 }
 
 // combine of G per-block summaries held in registers (summary b = lane + 64k):
-// two-pass semantics of the oracle.  Returns the winning summary's candidate,
-// or -1 - b when summary b is the first inside the band but its own candidate
-// is not (rare: rescan b's slice).
+// two-pass semantics of the oracle.  The first summary inside the band is the
+// lowest lane of the first k whose ballot is non-empty.  Returns the winning
+// summary's candidate, or -1 - b when summary b is the first inside the band
+// but its own candidate is not (rare: rescan b's slice).
 template <int NR>
 __device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[NR],
-                                    const double (&q)[NR], unsigned G, double thr, long long *sl,
-                                    long long *s_sel)
+                                    const double (&q)[NR], unsigned G, double thr)
 {
-    long long mine = NONE;       // first summary of this thread inside the band
-    int kmine = -1;
 #pragma unroll
-    for (int k = NR - 1; k >= 0; --k) {
-        const unsigned b = threadIdx.x + k * blockDim.x;
-        if (b < G && l[k] <= thr) { mine = b; kmine = k; }
+    for (int k = 0; k < NR; ++k) {
+        const unsigned b = threadIdx.x + k * GROUP_THREADS;
+        const u64 mask = __ballot(b < G && l[k] <= thr);
+        if (mask) {
+            const int f = __builtin_ctzll(mask);
+            const long long bsel = (long long)k * GROUP_THREADS + f;
+            const double qs = mk_d(__builtin_amdgcn_readlane(lo32(q[k]), f),
+                                   __builtin_amdgcn_readlane(hi32(q[k]), f));
+            const long long is = ((long long)(unsigned)__builtin_amdgcn_readlane((int)(i[k] >> 32), f) << 32) |
+                                 (unsigned)__builtin_amdgcn_readlane((int)i[k], f);
+            return qs <= thr ? is : -1 - bsel;
+        }
     }
-    long long bsel;
-    if constexpr (NR == 1) {     // summary b is lane b: the lowest lane in the band
-        const u64 mask = __ballot(mine != NONE);
-        bsel = mask ? (long long)__builtin_ctzll(mask) : NONE;
-    } else {
-        bsel = block_min_ll(mine, sl);
-    }
-    if (bsel == NONE) return NONE;
-    if (mine == bsel) {
-        s_sel[0] = q[kmine] <= thr ? i[kmine] : -1 - bsel;
-    }
-    __syncthreads();
-    return s_sel[0];
+    return NONE;
 }
 
-constexpr int IPL = 4;   // own columns per lane kept in registers
 constexpr int CH = 8;    // deferred pivots applied per chunk (loads issued together)
 
-// NR = summaries per lane (G <= 64 NR)
-template <int NR>
+// NR = summaries per lane (G <= 64 NR); IPL = own columns per lane (cpb <= 64 IPL)
+template <int NR, int IPL>
 __global__ void __launch_bounds__(GROUP_THREADS)
-k_group(Args A, int grp, int count, int from_erec, unsigned seq)
+k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
 {
     __shared__ double sd[16];
     __shared__ long long sl[16];
-    __shared__ long long sR[BMAX];     // local pivot rows of this group
-    __shared__ double sPc[BMAX];       // P[s][C] for the current entering column
-    __shared__ double sMr[BMAX];       // M[R][s] for the current leaving row
-    __shared__ long long s_sel[2];
-    __shared__ long long sRp[BMAX];    // previous group (lag): local pivot rows
-    __shared__ double sPcp[BMAX];      //   P'[s][C]
-    __shared__ double sMrp[BMAX];      //   M'[R][s]
-    // dynamic LDS: this block's rows' multipliers, its columns' pivot-row
-    // slices and its slices of row 0 / column 0 (own data never leaves LDS
-    // for a re-read; it is also published for the other blocks and the sweep)
+    __shared__ long long sR[BMAX + CH];     // local pivot rows of this group
+    __shared__ double sPc[BMAX + CH];       // P[s][C] for the current entering column
+    __shared__ double sMr[BMAX + CH];       // M[R][s] for the current leaving row
+    __shared__ long long sRp[BMAX + CH];    // previous group (lag): local pivot rows
+    __shared__ double sPcp[BMAX + CH];      //   P'[s][C]
+    __shared__ double sMrp[BMAX + CH];      //   M'[R][s]
+    // dynamic LDS, per own row / own column contiguous over the pivots with an
+    // odd stride cs (lanes 2-way over the banks; a chunk of pivots is one base
+    // address plus immediate offsets): this block's rows' multipliers, its
+    // columns' pivot-row values, its slices of row 0 / column 0, and with a
+    // lagging previous group its multipliers and pivot-row values too.  Own
+    // data never leaves LDS for a re-read; it is also published for the other
+    // blocks and the sweep.
     extern __shared__ __attribute__((aligned(16))) double dyn[];
     Ctl *ctl = A.ctl;
     const unsigned G = gridDim.x, b = blockIdx.x;
     const int tid = threadIdx.x;
-    const int nth = blockDim.x;
+    constexpr int nth = GROUP_THREADS;
     // this parity's previous sweep is complete (the host orders it); the
     // other parity holds the previous group, whose sweep may still be running
     const int np = A.lag ? (int)ctl->ndef[grp ^ 1] : 0;
@@ -841,21 +838,34 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
     u64 *grE = A.gran + GROUP_MAXBLOCKS * 8;   // row-0 summaries [G][8]
     const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= nth)
     const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
-    const long long cpb = (A.ld + G - 1) / G;               // columns per block
+    const long long cpb = (A.ld + G - 1) / G;               // columns per block (<= IPL nth)
     const long long jc0 = b * cpb, jc1 = min(jc0 + cpb, A.ld);
-    double *lM = dyn;                        // [count][rpb] (pivot-major: lanes read consecutive words)
-    double *lP = lM + rpb * count;           // [count][cpb]
-    double *l0 = lP + count * cpb;           // [cpb]  row 0 slice
-    double *lc = l0 + cpb;                   // [rpb]  column 0 slice
-    double *lMp = lc + rpb;                  // [np][rpb] previous group's multipliers (lag)
-    double *lPp = lMp + rpb * np;            // [np][cpb] previous group's pivot-row slices
+    const int cs = bmax + 1;
+    double *lM = dyn;                        // [rpb][cs]  M[own row][s]
+    double *lP = lM + rpb * cs;              // [cpb][cs]  P[s][own column]
+    double *l0 = lP + cpb * cs;              // [cpb]      row 0 slice
+    double *lc = l0 + cpb;                   // [rpb]      column 0 slice
+    double *lMp = lc + rpb;                  // [rpb][cs]  previous group (lag)
+    double *lPp = lMp + (np ? rpb * cs : 0); // [cpb][cs]
     const long long li = lr0 + tid;          // this lane's own row
     const bool own = li < lr1;
+    const long long kr = min((long long)tid, rpb - 1);
+    double *mrow = lM + kr * cs, *mrowp = lMp + kr * cs;
+    long long kc[IPL];                       // own columns jc0 + kc[k] (clamped into the slice)
+    const double *pcol[IPL], *pcolp[IPL];
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+        kc[k] = min((long long)tid + k * nth, cpb - 1);
+        pcol[k] = lP + kc[k] * cs;
+        pcolp[k] = lPp + kc[k] * cs;
+    }
     for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = A.row0[j];
     if (own) lc[tid] = A.col0[li];
+    u64 ownpiv = 0, ownpivp = 0;             // pivots s whose pivot row is this lane's row
     for (int s = 0; s < np; ++s) {
-        if (own) lMp[s * rpb + tid] = A.Mp[mi(A.rows, li, s)];
-        for (long long j = jc0 + tid; j < jc1; j += nth) lPp[s * cpb + (j - jc0)] = A.Pp[s * A.ld + j];
+        if (own) mrowp[s] = A.Mp[mi(A.rows, li, s)];
+        for (long long j = jc0 + tid; j < jc1; j += nth) lPp[(j - jc0) * cs + s] = A.Pp[s * A.ld + j];
+        if (A.dRp[s] == li) ownpivp |= 1ull << s;
     }
     if (tid < np) sRp[tid] = A.dRp[tid];
     const long long cap = ctl->cap;
@@ -903,8 +913,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
                         emin = fmin(emin, el[k]);
                     }
                 }
-                const long long rr = tid == 0 ? ld_sc1(&A.erec[0].rule) : 0;
-                rule = (int)__shfl(rr, 0, 64);
+                rule = (int)__builtin_amdgcn_readfirstlane((int)ld_sc1(&A.erec[0].rule));
             } else {
                 unsigned w[NR][NGE];
                 if (!gather<NR, NGE>(grE, G, gtag(seq, t - 1, 1), w, &ctl->bar_timeout)) {
@@ -941,7 +950,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
                     C = NONE;
                 } else {
                     const double ethr = tie_band(g, A.tol.cost_tie);
-                    C = combine_loaded(el, ei, eq, G, ethr, sl, s_sel);
+                    C = combine_loaded(el, ei, eq, G, ethr);
                     if (C < 0) {   // rare: rescan that slice of row 0
                         const long long k0 = (-1 - C) * cpb;
                         long long best = NONE;
@@ -956,7 +965,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         stamp(A, t, 1);
         if (pending >= 0) {
             if (own) {
-                const double c0 = upd(li, pendR, lM[pending * rpb + tid], p0, lc[tid]);
+                const double c0 = upd(li, pendR, mrow[pending], p0, lc[tid]);
                 lc[tid] = c0;
                 st_sc1(&A.col0[li], c0);
             }
@@ -976,29 +985,35 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         __syncthreads();
         stamp(A, t, 3);
         // deferred pivots on the own row's element of column C: the previous
-        // group's (lag), then this group's 0..t-1, CH at a time
-        auto chain_col = [&](int nt, const long long *sr, const double *spc, const double *lm) {
+        // group's (lag), then this group's 0..t-1, CH at a time.  A lane whose
+        // row was an earlier pivot row takes the select; otherwise plain FMAs.
+        auto chain_col = [&](int nt, const double *spc, const double *m, u64 piv) {
+            const u64 live = nt >= 64 ? ~0ull : (1ull << nt) - 1;
+            const bool sel = __ballot(own && (piv & live)) != 0;
             for (int s0 = 0; s0 < nt; s0 += CH) {
-                long long rr[CH];
                 double pc[CH], mm[CH];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
-                    const int s = min(s0 + u, nt - 1);
-                    rr[u] = sr[s];
-                    pc[u] = spc[s];
-                    mm[u] = lm[s * rpb + min((long long)tid, rpb - 1)];
+                    pc[u] = spc[s0 + u];
+                    mm[u] = m[s0 + u];
                 }
+                if (!sel) {
 #pragma unroll
-                for (int u = 0; u < CH; ++u)
-                    if (s0 + u < nt) a = upd(li, rr[u], mm[u], pc[u], a);
+                    for (int u = 0; u < CH; ++u)
+                        if (s0 + u < nt) a = fma(-mm[u], pc[u], a);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < CH; ++u)
+                        if (s0 + u < nt) a = ((piv >> (s0 + u)) & 1) ? pc[u] : fma(-mm[u], pc[u], a);
+                }
             }
         };
-        chain_col(np, sRp, sPcp, lMp);
-        chain_col(t, sR, sPc, lM);
+        chain_col(np, sPcp, mrowp, ownpivp);
+        chain_col(t, sPc, mrow, ownpiv);
         double qown = 0.0;
         bool okown = false;
         if (own) {
-            lM[t * rpb + tid] = a;
+            mrow[t] = a;
             st_sc1(&A.M[mi(A.rows, li, t)], a);
             qown = row_ratio(a, lc[tid], A.tol, okown);
         }
@@ -1053,7 +1068,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         const double g = block_min(rmin, sd);
         if (!(g < INFINITY)) { status = LP_UNBOUNDED; break; }
         const double thr = tie_band(g, A.tol.ratio_tie);
-        long long R = combine_loaded(rl, ri, rq, G, thr, sl, s_sel);
+        long long R = combine_loaded(rl, ri, rq, G, thr);
         if (R < 0) {   // rare: rescan the selected block's rows (their M[t], col0 are published)
             const long long bsel = -1 - R;
             const long long r0 = 1 + bsel * rpb, r1 = min(r0 + rpb, A.rows);
@@ -1065,6 +1080,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
             }
             R = block_min_ll(mine, sl);
         }
+        if (li == R) ownpiv |= 1ull << t;
         stamp(A, t, 7);
         // ---- pivot row on own columns, row 0 on own columns.  Tableau row
         //      loads first, then the cross-block loads (one round trip).
@@ -1078,71 +1094,51 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, R, tid)];
         if (tid == 0) sR[t] = R;
         const double f0 = ld_sc1(&A.M[mi(A.rows, 0, t)]);
+        // pivots s whose pivot row is R: the select instead of the FMA (uniform)
+        const u64 rpiv = __ballot(tid < t && sR[tid] == R);
+        const u64 rpivp = __ballot(tid < np && sRp[tid] == R);
         __syncthreads();
         stamp(A, t, 8);
         const double av = sMr[t];
-        // deferred pivots 0..t-1 of the group on the own columns, CH at a time
-        auto chain1 = [&](double (&x)[IPL], long long kbase, int nt, const long long *sr,
-                          const double *smr, const double *lp) {
+        // deferred pivots of the previous group (lag), then 0..t-1 of this
+        // group, on the own columns, CH at a time
+        auto chain_row = [&](int nt, const double *smr, const double *const (&pc)[IPL], u64 piv) {
             for (int s0 = 0; s0 < nt; s0 += CH) {
-                long long rr[CH];
                 double mr[CH], pv[CH][IPL];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
-                    const int s = min(s0 + u, nt - 1);
-                    rr[u] = sr[s];
-                    mr[u] = smr[s];
+                    mr[u] = smr[s0 + u];
 #pragma unroll
-                    for (int k = 0; k < IPL; ++k)
-                        pv[u][k] = lp[s * cpb + min(kbase + k * nth, cpb - 1)];
+                    for (int k = 0; k < IPL; ++k) pv[u][k] = pc[k][s0 + u];
                 }
 #pragma unroll
                 for (int u = 0; u < CH; ++u)
                     if (s0 + u < nt) {
-                        if (R == rr[u]) {          // row R was pivot row s
+                        if ((piv >> (s0 + u)) & 1) {     // row R was pivot row s
 #pragma unroll
-                            for (int k = 0; k < IPL; ++k) x[k] = pv[u][k];
+                            for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
                         } else {
 #pragma unroll
-                            for (int k = 0; k < IPL; ++k) x[k] = fma(-mr[u], pv[u][k], x[k]);
+                            for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
                         }
                     }
             }
         };
-        auto chain = [&](double (&x)[IPL], long long kbase) {
-            chain1(x, kbase, np, sRp, sMrp, lPp);
-            chain1(x, kbase, t, sR, sMr, lP);
-        };
+        chain_row(np, sMrp, pcolp, rpivp);
+        chain_row(t, sMr, pcol, rpiv);
         double vmin = INFINITY, v0 = 0.0;
-        auto finish_col = [&](long long j, double x) {
-            const long long k = j - jc0;
-            const double p = (j == C) ? 1.0 : x / av;
-            lP[t * cpb + k] = p;
-            st_sc1(&A.P[t * A.ld + j], p);
-            const double v = upd(0, -1, f0, p, l0[k]);
-            l0[k] = v;
-            st_sc1(&A.row0[j], v);
-            if (j == 0) v0 = v;
-            if (j >= 1 && j <= A.n) vmin = fmin(vmin, v);
-        };
-        chain(xv, tid);
 #pragma unroll
-        for (int k2 = 0; k2 < IPL; ++k2) {
-            const long long j = jc0 + tid + k2 * nth;
-            if (j < jc1) finish_col(j, xv[k2]);
-        }
-        for (long long j0 = jc0 + IPL * nth; j0 < jc1; j0 += IPL * nth) {   // wide slices
-            double x2[IPL];
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) {
-                const long long j = j0 + tid + k * nth;
-                x2[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
-            }
-            chain(x2, j0 - jc0 + tid);
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) {
-                const long long j = j0 + tid + k * nth;
-                if (j < jc1) finish_col(j, x2[k]);
+        for (int k = 0; k < IPL; ++k) {
+            const long long j = jc0 + tid + k * nth;
+            if (j < jc1) {
+                const double p = (j == C) ? 1.0 : xv[k] / av;
+                lP[kc[k] * cs + t] = p;
+                st_sc1(&A.P[t * A.ld + j], p);
+                const double v = upd(0, -1, f0, p, l0[kc[k]]);
+                l0[kc[k]] = v;
+                st_sc1(&A.row0[j], v);
+                if (j == 0) v0 = v;
+                if (j >= 1 && j <= A.n) vmin = fmin(vmin, v);
             }
         }
         __syncthreads();
@@ -1199,7 +1195,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
             }
         }
         rule = __builtin_amdgcn_readfirstlane(rule);   // block 0 lane 0 may have switched it
-        const double p0n = b == 0 ? lP[t * cpb] : 0.0;     // P[t][0] (column 0 is block 0's)
+        const double p0n = b == 0 ? lP[t] : 0.0;       // P[t][0] (column 0 is block 0's first)
         if (t == count - 1) {         // the next launch reads plain summaries
             if (tid == 0) {
                 st_sc1(&A.erec[b].l, el);
@@ -1233,7 +1229,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq)
         if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout)) {
             const double pl = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
                                    __builtin_amdgcn_readfirstlane(w[0][7]));
-            if (own) st_sc1(&A.col0[li], upd(li, pendR, lM[pending * rpb + tid], pl, lc[tid]));
+            if (own) st_sc1(&A.col0[li], upd(li, pendR, mrow[pending], pl, lc[tid]));
         } else {
             status = LP_DEVICE_ERROR;
         }
@@ -1463,15 +1459,20 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
     if (g == 0) return hipErrorInvalidValue;
     const size_t lds = (size_t)group_lds(A.rc, A.ld, g, bmax, A.lag);
     const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
-    if (nr <= 1)
-        hipLaunchKernelGGL(k_group<1>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp,
-                           count, from_erec, seq);
-    else if (nr <= 2)
-        hipLaunchKernelGGL(k_group<2>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A, grp,
-                           count, from_erec, seq);
-    else
-        hipLaunchKernelGGL(k_group<NRMAX>, dim3((unsigned)g), dim3(GROUP_THREADS), lds, s, A,
-                           grp, count, from_erec, seq);
+    const int ipl = (int)(((A.ld + g - 1) / g + GROUP_THREADS - 1) / GROUP_THREADS);
+#define GROUP_LAUNCH(NRV, IPLV)                                                               \
+    hipLaunchKernelGGL((k_group<NRV, IPLV>), dim3((unsigned)g), dim3(GROUP_THREADS), lds, s,  \
+                       A, grp, count, from_erec, seq, bmax)
+    if (ipl <= 2) {
+        if (nr <= 1) GROUP_LAUNCH(1, 2);
+        else if (nr <= 2) GROUP_LAUNCH(2, 2);
+        else GROUP_LAUNCH(NRMAX, 2);
+    } else {
+        if (nr <= 1) GROUP_LAUNCH(1, 4);
+        else if (nr <= 2) GROUP_LAUNCH(2, 4);
+        else GROUP_LAUNCH(NRMAX, 4);
+    }
+#undef GROUP_LAUNCH
     return hipGetLastError();
 }
 
