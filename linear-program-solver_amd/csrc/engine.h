@@ -149,7 +149,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 // seq numbers the launches of a handle (1 .. 2^26-1, then wraps to 1): it tags
 // the launch's summaries so no stale granule can match
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax);
+                        unsigned seq, int bmax, int lag_layout);
 #ifndef LPK_GROUP_BLOCKS
 #define LPK_GROUP_BLOCKS 64
 #endif

@@ -754,17 +754,17 @@ __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[
                        unsigned *timeout_flag)
 {
     for (unsigned spins = 0;; ++spins) {
+        // every load is issued before any is waited for: lanes past the last
+        // block re-read block G-1 (in bounds, already tagged) and ignore it
         bool ok = true;
 #pragma unroll
         for (int k = 0; k < NR; ++k) {
-            const unsigned bb = threadIdx.x + k * GROUP_THREADS;
-            if (bb < G) {
+            const unsigned bb = min(threadIdx.x + k * GROUP_THREADS, G - 1);
 #pragma unroll
-                for (int g = 0; g < NG; ++g) {
-                    const u64 v = ld_sc1(&base[bb * 8 + g]);
-                    w[k][g] = (unsigned)v;
-                    ok = ok && (unsigned)(v >> 32) == tag;
-                }
+            for (int g = 0; g < NG; ++g) {
+                const u64 v = ld_sc1(&base[bb * 8 + g]);
+                w[k][g] = (unsigned)v;
+                ok = ok && (unsigned)(v >> 32) == tag;
             }
         }
         if (__all(ok)) return true;
@@ -1452,12 +1452,14 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 }
 
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax)
+                        unsigned seq, int bmax, int lag_layout)
 {
-    if (count < 1 || count > bmax || bmax > BMAX) return hipErrorInvalidValue;
-    const long long g = group_blocks(A.rc, A.ld, bmax, A.lag);
+    if (count < 1 || count > bmax || bmax > BMAX || (A.lag && !lag_layout)) return hipErrorInvalidValue;
+    // every launch of a chain must have the same geometry (the next one reads
+    // the plain per-block summaries this one leaves): sized by lag_layout
+    const long long g = group_blocks(A.rc, A.ld, bmax, lag_layout);
     if (g == 0) return hipErrorInvalidValue;
-    const size_t lds = (size_t)group_lds(A.rc, A.ld, g, bmax, A.lag);
+    const size_t lds = (size_t)group_lds(A.rc, A.ld, g, bmax, lag_layout);
     const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
     const int ipl = (int)(((A.ld + g - 1) / g + GROUP_THREADS - 1) / GROUP_THREADS);
 #define GROUP_LAUNCH(NRV, IPLV)                                                               \

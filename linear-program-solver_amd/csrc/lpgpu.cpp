@@ -727,7 +727,9 @@ static int ensure_pipeline(lp_handle *h, long long g)
     }
     int ncu = 0;
     HCHK(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev));
-    int nsel = h->sel_cus > 0 ? h->sel_cus : (int)std::min<long long>(g, ncu / 4);
+    // one selection block per CU where possible (all G blocks must be
+    // co-resident on the selection CUs)
+    int nsel = h->sel_cus > 0 ? h->sel_cus : (int)std::min<long long>(g, ncu / 2);
     nsel = std::max(1, std::min(nsel, ncu / 2));
     std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mw((ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; ++c) (c < nsel ? ms : mw)[c / 32] |= 1u << (c % 32);
@@ -773,7 +775,7 @@ static int enqueue_pipelined(lp_handle *h, int64_t b, bool &chained, int *ngroup
         Args A = args_par(h, par, buf[gi == 0 ? 0 : (gi - 1) & 1], gi > 0 ? 1 : 0);
         if (gi >= 2) HCHK(h, hipStreamWaitEvent(h->ssel, esw[gi - 2], 0));
         h->gseq = h->gseq % ((1u << 26) - 1) + 1;
-        HCHK(h, lpk::launch_group(h->ssel, A, par, cnt, chained ? 1 : 0, h->gseq, B));
+        HCHK(h, lpk::launch_group(h->ssel, A, par, cnt, chained ? 1 : 0, h->gseq, B, 1));
         CALL(pev_at(h, ne++, &esel));
         HCHK(h, hipEventRecord(esel, h->ssel));
         last_sel = esel;
@@ -834,7 +836,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             for (int64_t k = 0; k < b; k += B) {
                 const int cnt = (int)std::min<int64_t>(B, b - k);
                 h->gseq = h->gseq % ((1u << 26) - 1) + 1;
-                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0, h->gseq, B));
+                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0, h->gseq, B, 0));
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
                 chained = true;
