@@ -718,6 +718,12 @@ __device__ __forceinline__ void stamp(const Args &A, int t, int k)
     if (A.stamps && blockIdx.x == 0 && threadIdx.x == 0 && t < BMAX)
         A.stamps[t * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
+// every block: when it published its ratio (k = 0) / row-0 (k = 1) summary
+__device__ __forceinline__ void bstamp(const Args &A, int t, int k)
+{
+    if (A.stamps && threadIdx.x == 0 && t < BMAX)
+        A.stamps[BMAX * 16 + (blockIdx.x * BMAX + t) * 2 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
 
 typedef unsigned long long u64;
 constexpr int NRMAX = (GROUP_MAXBLOCKS + GROUP_THREADS - 1) / GROUP_THREADS;
@@ -749,6 +755,11 @@ __device__ __forceinline__ void publish(u64 *slot, unsigned tag, unsigned w, int
 
 // every block's summary, lane l holding blocks l + 64k; polls until every
 // granule carries `tag`.  Bounded (a never-expected timeout flags the ctl).
+// every block's summary, lane l holding blocks l + 64k; polls until every
+// granule carries `tag`.  Bounded (a never-expected timeout flags the ctl).
+// (Keeping a second poll in flight was measured: the gather ends sooner but
+// the leftover loads delay the next phase's loads by as much -- vmcnt retires
+// in order.)
 template <int NR, int NG>
 __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[NR][NG],
                        unsigned *timeout_flag)
@@ -1038,6 +1049,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
             else if (tid == 3) wv = hi32(qb);
             publish(&grR[b * 8], gtag(seq, t, 0), wv, NGR);
         }
+        bstamp(A, t, 0);
         stamp(A, t, 5);
 
         // ---- leaving row (combine the ratio summaries)
@@ -1217,6 +1229,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
             else if (tid == 7) wv = hi32(p0n);
             publish(&grE[b * 8], gtag(seq, t, 1), wv, NGE);
         }
+        bstamp(A, t, 1);
         ++npiv;
         stamp(A, t, 11);
         pending = t;
@@ -1250,14 +1263,15 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
 //   pivot rows take a select per row.  Each element is loaded and stored once.
 // ---------------------------------------------------------------------------
 
-template <int SWEEP_WAVES, int SWEEP_RW, int SWEEP_NG>
-__global__ void __launch_bounds__(64 * SWEEP_WAVES)
+template <int SW_WAVES, int SW_RW, bool MLDS>
+__global__ void __launch_bounds__(64 * SW_WAVES)
 k_sweep(const double *T, double *Tout, const double *__restrict__ P,
         const double *__restrict__ M, const long long *__restrict__ dR,
         const Ctl *__restrict__ ctl, long long ld, long long rows, int grp)
 {
-    constexpr int SWEEP_ROWS = SWEEP_WAVES * SWEEP_RW * SWEEP_NG;
+    constexpr int ROWS = SW_WAVES * SW_RW;     // rows per block
     __shared__ double2 sp[BMAX][64];          // the block's 128-column slice of P
+    __shared__ double sm[MLDS ? BMAX : 1][MLDS ? ROWS : 1];   // its rows' multipliers
     __shared__ long long sr[BMAX];            // pivot rows
     const int nd = (int)ctl->ndef[grp];
     if (nd == 0) return;
@@ -1265,74 +1279,72 @@ k_sweep(const double *T, double *Tout, const double *__restrict__ P,
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long j0 = (long long)blockIdx.x * 128 + lane * 2;
     const bool active = j0 < ld;
-    for (int s = wave; s < nd; s += SWEEP_WAVES)
+    const long long base = (long long)blockIdx.y * ROWS;
+    for (int s = wave; s < nd; s += SW_WAVES)
         sp[s][lane] = active ? *reinterpret_cast<const double2 *>(P + s * ld + j0)
                              : make_double2(0.0, 0.0);
-    if (threadIdx.x < nd) sr[threadIdx.x] = dR[threadIdx.x];
-    const long long base = (long long)blockIdx.y * SWEEP_ROWS;
-    // row group g of this wave: rows [rb(g), rb(g) + SWEEP_RW)
-    auto rb_of = [&](int g) { return base + (long long)(g * SWEEP_WAVES + wave) * SWEEP_RW; };
-    // rows past the end re-load the last row (in bounds) and are not stored
-    auto load = [&](double2 (&x)[SWEEP_RW], long long rb) {
-        if (!active || rb >= rows) return;
-#pragma unroll
-        for (int k = 0; k < SWEEP_RW; ++k)
-            x[k] = *reinterpret_cast<const double2 *>(T + min(rb + k, rows - 1) * ld + j0);
-    };
-    auto apply = [&](double2 (&x)[SWEEP_RW], long long rb) {
-        if (!active || rb >= rows) return;
-        const long long nr = min((long long)SWEEP_RW, rows - rb);
-        bool pivrow_here = false;
-        for (int s = 0; s < nd; ++s) {
-            const long long R = sr[s];
-            pivrow_here |= (R >= rb && R < rb + nr);
+    if constexpr (MLDS) {
+        // M is pivot-major: a pivot's multipliers of the block's rows are
+        // contiguous (rows past the end read the padding after M)
+        for (int idx = threadIdx.x; idx < nd * ROWS; idx += 64 * SW_WAVES) {
+            const int s = idx / ROWS, k = idx % ROWS;
+            sm[s][k] = M[s * rows + base + k];
         }
-        const double *mt = M + rb;             // M[s * rows + rb + k]
-        if (!pivrow_here) {
-#pragma unroll 2
-            for (int s = 0; s < nd; ++s) {
-                const double2 pv = sp[s][lane];
-                const double *f = mt + s * rows;
-                double fk[SWEEP_RW];
-#pragma unroll
-                for (int k = 0; k < SWEEP_RW; ++k) fk[k] = f[k];
-#pragma unroll
-                for (int k = 0; k < SWEEP_RW; ++k) {
-                    x[k].x = fma(-fk[k], pv.x, x[k].x);
-                    x[k].y = fma(-fk[k], pv.y, x[k].y);
-                }
-            }
-        } else {
-            for (int s = 0; s < nd; ++s) {
-                const double2 pv = sp[s][lane];
-                const double *f = mt + s * rows;
-                const long long kr = sr[s] - rb;   // this pivot's row in the group, if any
-#pragma unroll
-                for (int k = 0; k < SWEEP_RW; ++k) {
-                    const double fk = f[k];
-                    if (k == kr) {
-                        x[k] = pv;
-                    } else {
-                        x[k].x = fma(-fk, pv.x, x[k].x);
-                        x[k].y = fma(-fk, pv.y, x[k].y);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < SWEEP_RW; ++k)
-            if (k < nr) *reinterpret_cast<double2 *>(Tout + (rb + k) * ld + j0) = x[k];
-    };
-    // software pipeline over the wave's row groups: group g+1 is in flight
-    // while group g is updated
-    double2 x[2][SWEEP_RW];
-    load(x[0], rb_of(0));
-    __syncthreads();
-#pragma unroll
-    for (int g = 0; g < SWEEP_NG; ++g) {
-        if (g + 1 < SWEEP_NG) load(x[(g + 1) & 1], rb_of(g + 1));
-        apply(x[g & 1], rb_of(g));
     }
+    if (threadIdx.x < nd) sr[threadIdx.x] = dR[threadIdx.x];
+    const long long rb = base + (long long)wave * SW_RW;
+    // rows past the end re-load the last row (in bounds) and are not stored
+    double2 x[SW_RW];
+    if (active && rb < rows) {
+#pragma unroll
+        for (int k = 0; k < SW_RW; ++k)
+            x[k] = *reinterpret_cast<const double2 *>(T + min(rb + k, rows - 1) * ld + j0);
+    }
+    __syncthreads();
+    if (!active || rb >= rows) return;
+    const long long nr = min((long long)SW_RW, rows - rb);
+    bool pivrow_here = false;
+    for (int s = 0; s < nd; ++s) {
+        const long long R = sr[s];
+        pivrow_here |= (R >= rb && R < rb + nr);
+    }
+    const double *mt = M + rb;                 // M[s * rows + rb + k]
+    auto mult = [&](int s, int k) -> double {
+        if constexpr (MLDS) return sm[s][wave * SW_RW + k];
+        else return mt[s * rows + k];
+    };
+    if (!pivrow_here) {
+#pragma unroll 2
+        for (int s = 0; s < nd; ++s) {
+            const double2 pv = sp[s][lane];
+            double fk[SW_RW];
+#pragma unroll
+            for (int k = 0; k < SW_RW; ++k) fk[k] = mult(s, k);
+#pragma unroll
+            for (int k = 0; k < SW_RW; ++k) {
+                x[k].x = fma(-fk[k], pv.x, x[k].x);
+                x[k].y = fma(-fk[k], pv.y, x[k].y);
+            }
+        }
+    } else {
+        for (int s = 0; s < nd; ++s) {
+            const double2 pv = sp[s][lane];
+            const long long kr = sr[s] - rb;   // this pivot's row in the group, if any
+#pragma unroll
+            for (int k = 0; k < SW_RW; ++k) {
+                const double fk = mult(s, k);
+                if (k == kr) {
+                    x[k] = pv;
+                } else {
+                    x[k].x = fma(-fk, pv.x, x[k].x);
+                    x[k].y = fma(-fk, pv.y, x[k].y);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < SW_RW; ++k)
+        if (k < nr) *reinterpret_cast<double2 *>(Tout + (rb + k) * ld + j0) = x[k];
 }
 
 __global__ void k_resume(Ctl *ctl)
@@ -1433,19 +1445,17 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
         variant = 0;
         if (const char *v = getenv("LPGPU_SWEEP")) variant = atoi(v);
     }
-#define SWEEP_LAUNCH(W, RW, NG)                                                              \
-    hipLaunchKernelGGL((k_sweep<W, RW, NG>),                                                 \
+#define SWEEP_LAUNCH(W, RW, ML)                                                              \
+    hipLaunchKernelGGL((k_sweep<W, RW, ML>),                                                 \
                        dim3((unsigned)((A.ld + 127) / 128),                                  \
-                            (unsigned)((A.rows + W * RW * NG - 1) / (W * RW * NG))),         \
+                            (unsigned)((A.rows + W * RW - 1) / (W * RW))),                   \
                        dim3(64 * W), 0, s, A.T, T_out, A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp)
     switch (variant) {
-    case 1: SWEEP_LAUNCH(4, 8, 2); break;
-    case 2: SWEEP_LAUNCH(8, 8, 2); break;
-    case 3: SWEEP_LAUNCH(8, 8, 4); break;
-    case 4: SWEEP_LAUNCH(4, 16, 1); break;
-    case 5: SWEEP_LAUNCH(4, 8, 4); break;
-    case 6: SWEEP_LAUNCH(2, 8, 4); break;
-    default: SWEEP_LAUNCH(8, 8, 1); break;
+    case 1: SWEEP_LAUNCH(8, 8, false); break;
+    case 2: SWEEP_LAUNCH(4, 8, true); break;
+    case 3: SWEEP_LAUNCH(8, 4, true); break;
+    case 5: SWEEP_LAUNCH(8, 8, true); break;
+    default: SWEEP_LAUNCH(16, 4, true); break;
     }
 #undef SWEEP_LAUNCH
     return hipGetLastError();

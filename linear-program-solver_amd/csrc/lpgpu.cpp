@@ -267,8 +267,9 @@ static int alloc_handle(lp_handle *h)
     if (const char *sc = std::getenv("LPGPU_SEL_CUS")) h->sel_cus = std::atoi(sc);
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
-            HCHK(h, hipMalloc(&h->stamps, lpk::BMAX * 16 * sizeof(long long)));
-            HCHK(h, hipMemset(h->stamps, 0, lpk::BMAX * 16 * sizeof(long long)));
+            const size_t sb = (lpk::BMAX * 16 + lpk::GROUP_MAXBLOCKS * lpk::BMAX * 2) * sizeof(long long);
+            HCHK(h, hipMalloc(&h->stamps, sb));
+            HCHK(h, hipMemset(h->stamps, 0, sb));
         }
     HCHK(h, hipSetDevice(h->dev));
     if (!h->s) HCHK(h, hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking));
@@ -731,8 +732,15 @@ static int ensure_pipeline(lp_handle *h, long long g)
     // co-resident on the selection CUs)
     int nsel = h->sel_cus > 0 ? h->sel_cus : (int)std::min<long long>(g, ncu / 2);
     nsel = std::max(1, std::min(nsel, ncu / 2));
+    // the sweep may be held to fewer CUs (LPGPU_SWEEP_CUS): less bandwidth for
+    // it, less contention for the latency-bound selection beside it
+    int nsw = ncu - nsel;
+    if (const char *sw = std::getenv("LPGPU_SWEEP_CUS")) nsw = std::max(1, std::min(nsw, std::atoi(sw)));
     std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mw((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) (c < nsel ? ms : mw)[c / 32] |= 1u << (c % 32);
+    for (int c = 0; c < ncu; ++c) {
+        if (c < nsel) ms[c / 32] |= 1u << (c % 32);
+        else if (c < nsel + nsw) mw[c / 32] |= 1u << (c % 32);
+    }
     HCHK(h, hipExtStreamCreateWithCUMask(&h->ssel, (uint32_t)ms.size(), ms.data()));
     HCHK(h, hipExtStreamCreateWithCUMask(&h->ssw, (uint32_t)mw.size(), mw.data()));
     h->sel_cus = nsel;
@@ -975,6 +983,14 @@ extern "C" int lp_update_time(lp_handle *h, double *ms, int64_t *launches)
 }
 
 // diagnostic (not part of the C-ABI): k_group phase clocks of the last group
+extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
+{
+    if (!h->stamps) return LP_BAD_ARG;
+    HCHK(h, hipMemcpy(out, h->stamps + lpk::BMAX * 16,
+                      lpk::GROUP_MAXBLOCKS * lpk::BMAX * 2 * sizeof(long long), hipMemcpyDeviceToHost));
+    return LP_PIVOTED;
+}
+
 extern "C" int lpdiag_stamps(lp_handle *h, long long *out)
 {
     if (!h->stamps) return LP_BAD_ARG;

@@ -27,3 +27,23 @@ for t in range(15):
     print(t, " ".join(f"{n}={x:4.2f}" for n, x in zip(names, d)))
 avg = [sum(r[k] for r in rows[1:]) / (len(rows) - 1) for k in range(len(names))]
 print("avg", " ".join(f"{n}={x:4.2f}" for n, x in zip(names, avg)), "sum", round(sum(avg), 2))
+
+# per-block publish times: spread across blocks and the last blocks
+G = 65
+bb = (C.c_longlong * (256 * 32 * 2))()
+assert e.lib.lpdiag_bstamps(e.h, bb) == 0
+spread = [[], []]
+last = {}
+for t in range(1, 15):
+    for k in (0, 1):
+        v = [bb[(b * 32 + t) * 2 + k] for b in range(G)]
+        v = [x for x in v if x]
+        if not v:
+            continue
+        spread[k].append((max(v) - min(v)) * 10 / 1000)
+        order = sorted(range(len(v)), key=lambda i: v[i])
+        for b in order[-3:]:
+            last[(k, b)] = last.get((k, b), 0) + 1
+print("publish spread us: ratio avg %.2f max %.2f | row0 avg %.2f max %.2f" % (
+    sum(spread[0]) / len(spread[0]), max(spread[0]), sum(spread[1]) / len(spread[1]), max(spread[1])))
+print("most often among the last 3:", sorted(last.items(), key=lambda kv: -kv[1])[:10])

@@ -54,7 +54,7 @@ for step in "$@"; do
                 run bench_p_b$B 300 python bench.py --no-cpu-baseline --block $B
             done ;;
         sweepvar)
-            for V in 0 1 2 3 4 5 6; do
+            for V in ${SWEEP_VARIANTS:-0 1 2 3 4}; do
                 for B in 16 32; do
                     LPGPU_PIPELINE=0 LPGPU_SWEEP=$V run bench_v${V}_b$B 300 python bench.py --no-cpu-baseline --block $B --steps 512
                 done
@@ -74,6 +74,17 @@ for step in "$@"; do
                     LPGPU_PIPELINE=0 run bench_np_b${B}_$rep 300 python bench.py --no-cpu-baseline --steps 1024 --block $B
                     LPGPU_PIPELINE=1 run bench_p_b${B}_$rep 300 python bench.py --no-cpu-baseline --steps 1024 --block $B
                 done
+            done ;;
+        swcus)
+            LPGPU_PIPELINE=0 run bench_np 300 python bench.py --no-cpu-baseline --steps 1024
+            for C in 32 64 96 128 191; do
+                LPGPU_PIPELINE=1 LPGPU_SWEEP_CUS=$C run bench_p_sw$C 300 python bench.py --no-cpu-baseline --steps 1024
+            done ;;
+        pmcsq)
+            export TMPDIR=/tmp
+            for B in 16 32; do
+                run pmcsq_b$B 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_LDS --output-format csv -d "$OUT/pmcsq_b$B" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline --block $B
+                run pmcgr_b$B 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcgr_b$B" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline --block $B
             done ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
