@@ -129,6 +129,9 @@ def main():
                                                             "hbm_traffic.json"))
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU diagnostic: run the N-rank job's whole tableau on one GPU")
+    ap.add_argument("--group-shards", type=int, default=0,
+                    help="1-GPU diagnostic: the N-rank row-sharded job as N in-process shards "
+                         "on one GPU (device copies instead of RCCL)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -146,24 +149,31 @@ def main():
         import torch.distributed as dist  # plumbing only: uid exchange, barriers, max
         dist.init_process_group("gloo")
 
-    nsim = args.emulate_ranks if args.emulate_ranks else world
+    nsim = args.emulate_ranks or args.group_shards or world
     kind, m, ns, n, rb, re_ = workload(nsim, rank if world > 1 else 0)
     if world == 1:
         rb, re_ = 0, m
+    shards = None
     if world > 1:
         uid = _lib.comm_unique_id() if rank == 0 else None
         box = [uid]
         dist.broadcast_object_list(box, src=0)
         eng = _lib.create_sharded(m, n, rank, world, box[0], device=device)
         assert (eng.row_begin, eng.row_count) == (rb, re_ - rb)
+    elif args.group_shards:
+        shards = _lib.create_group(m, n, args.group_shards, device=device)
+        eng = shards[0]
+        rb, re_ = eng.row_begin, eng.row_begin + eng.row_count
     else:
         eng = _lib.Engine(m, n, device=device)
     eng.set_block(args.block)
-    eng.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
     blk = 2048
-    for a in range(rb, re_, blk):
-        b = min(a + blk, re_)
-        eng.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + b))
+    for e in (shards or [eng]):
+        e.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
+        a0, a1 = (e.row_begin, e.row_begin + e.row_count) if shards else (rb, re_)
+        for a in range(a0, a1, blk):
+            b = min(a + blk, a1)
+            e.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + b))
 
     def barrier():
         if dist is not None:
@@ -181,6 +191,7 @@ def main():
     if done != args.steps:
         raise SystemExit(f"timed run ended early: status {st} after {done} pivots")
     upd_ms, upd_n = eng.update_time()
+    sel_ms, sel_n = eng.select_time()
     eng.profile(False)
     elapsed = t1 - t0
     if dist is not None:
@@ -210,9 +221,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic (counter-based splitmix64 dyadic k/64 LP, lpsol_amd.generators)",
         "config": {
-            "workload": ("cfg3: 4096x8192 float64 tableau, G_mixed seed 3" if world == 1 else
+            "workload": ("cfg3: 4096x8192 float64 tableau, G_mixed seed 3" if nsim == 1 else
                          f"G_tall {m}x{n} float64 tableau seed 3, {ROWS_PER_GPU} rows per GPU"
-                         + (" (cfg4)" if world == 8 else "")),
+                         + (" (cfg4)" if nsim == 8 else "")
+                         + (f" [diagnostic: whole tableau on 1 GPU]" if args.emulate_ranks else "")
+                         + (f" [diagnostic: {nsim} in-process shards on 1 GPU]" if args.group_shards else "")),
             "m": m, "n": n, "rows_per_gpu": re_ - rb, "rule": "standard (findPivotStandard)",
             "parallelism": f"row-shard x{world}" + (" over RCCL" if world > 1 else ""),
         },
@@ -232,8 +245,20 @@ def main():
             "traffic": traffic,
             "bytes_per_launch": sweep_b,
             "avg_launch_us": upd_avg_ms * 1e3,
+            "time_share": upd_ms / (elapsed * 1e3),
         },
     }
+    if sel_n:
+        # the other kernel of the path: one persistent launch selects a group of
+        # pivots; its time is the chain of per-pivot summary exchanges and
+        # dependent loads (latency), not bytes
+        out["selection"] = {
+            "kernel": "k_group (persistent pivot selection, latency-bound)",
+            "avg_launch_us": 1e3 * sel_ms / sel_n,
+            "pivots_per_launch": args.block,
+            "us_per_pivot": 1e3 * sel_ms / sel_n / args.block,
+            "time_share": sel_ms / (elapsed * 1e3),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -147,6 +147,9 @@ int lp_get_block(const lp_handle *h, int *pivots_per_sweep);
  * the last reset. */
 int lp_profile(lp_handle *h, int enable);
 int lp_update_time(lp_handle *h, double *ms, int64_t *launches);
+/* The same for the pivot-selection launches (one per group of
+ * pivots_per_sweep pivots on the single-device path). */
+int lp_select_time(lp_handle *h, double *ms, int64_t *launches);
 
 /* Human-readable description of the last failure on this handle (or of the
  * last failed lp_create* when h is NULL). */

@@ -185,7 +185,8 @@ __host__ __device__ inline long long group_blocks(long long rc, long long ld, in
     if (g4 > g) g = g4;
     while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX) g *= 2;
     if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
-    if ((ld + g - 1) / g > 4 * GROUP_THREADS) return 0;
+    if ((ld + g - 1) / g > 4 * GROUP_THREADS) return 0;   // more than 4 columns per lane
+    if ((rc + g - 1) / g > GROUP_ROWS) return 0;          // more than one row per lane
     return group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX ? 0 : g;
 }
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);

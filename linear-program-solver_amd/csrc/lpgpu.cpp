@@ -64,8 +64,11 @@ struct lp_handle {
     bool prof = false;
     std::vector<hipEvent_t> ev;     // pairs (start, end) of update launches
     size_t evused = 0;
+    std::vector<int> evkind;        // per pair: 0 sweep, 1 selection (k_group)
     double prof_ms = 0.0;
     int64_t prof_n = 0;
+    double sel_ms = 0.0;            // k_group launches
+    int64_t sel_n = 0;
     int rank = 0, nranks = 1;
     std::shared_ptr<Comm> comm;     // null: single device, no exchange
     std::string err;
@@ -583,27 +586,48 @@ static int ensure_log(lp_handle *h, int64_t need)
     return LP_PIVOTED;
 }
 
-static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, hipStream_t st = nullptr,
-                              double *T_out = nullptr)
+// event pair around a launch on stream st when profiling (kind 0 sweep, 1 selection)
+static int prof_begin(lp_handle *h, hipStream_t st)
 {
-    if (!st) st = h->s;
-    if (!T_out) T_out = A.T;
-    if (!h->prof) {
-        HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out));
-        return LP_PIVOTED;
-    }
+    if (!h->prof) return LP_PIVOTED;
     if (h->evused + 2 > h->ev.size()) {
         hipEvent_t a, b;
         HCHK(h, hipEventCreate(&a));
         HCHK(h, hipEventCreate(&b));
         h->ev.push_back(a);
         h->ev.push_back(b);
+        h->evkind.push_back(0);
     }
     HCHK(h, hipEventRecord(h->ev[h->evused], st));
-    HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out));
+    return LP_PIVOTED;
+}
+
+static int prof_end(lp_handle *h, hipStream_t st, int kind)
+{
+    if (!h->prof) return LP_PIVOTED;
     HCHK(h, hipEventRecord(h->ev[h->evused + 1], st));
+    h->evkind[h->evused / 2] = kind;
     h->evused += 2;
     return LP_PIVOTED;
+}
+
+static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, hipStream_t st = nullptr,
+                              double *T_out = nullptr)
+{
+    if (!st) st = h->s;
+    if (!T_out) T_out = A.T;
+    CALL(prof_begin(h, st));
+    HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out));
+    return prof_end(h, st, 0);
+}
+
+static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int grp, int cnt,
+                              int from_erec, int lag_layout)
+{
+    h->gseq = h->gseq % ((1u << 26) - 1) + 1;
+    CALL(prof_begin(h, st));
+    HCHK(h, lpk::launch_group(st, A, grp, cnt, from_erec, h->gseq, h->block, lag_layout));
+    return prof_end(h, st, 1);
 }
 
 // after a stream sync: fold recorded sweep launches into the totals
@@ -612,8 +636,13 @@ static int collect_profile(lp_handle *h)
     for (size_t k = 0; k + 1 < h->evused; k += 2) {
         float ms = 0.f;
         HCHK(h, hipEventElapsedTime(&ms, h->ev[k], h->ev[k + 1]));
-        h->prof_ms += ms;
-        h->prof_n += 1;
+        if (h->evkind[k / 2] == 1) {
+            h->sel_ms += ms;
+            h->sel_n += 1;
+        } else {
+            h->prof_ms += ms;
+            h->prof_n += 1;
+        }
     }
     h->evused = 0;
     return LP_PIVOTED;
@@ -782,8 +811,7 @@ static int enqueue_pipelined(lp_handle *h, int64_t b, bool &chained, int *ngroup
         const int par = gi & 1;
         Args A = args_par(h, par, buf[gi == 0 ? 0 : (gi - 1) & 1], gi > 0 ? 1 : 0);
         if (gi >= 2) HCHK(h, hipStreamWaitEvent(h->ssel, esw[gi - 2], 0));
-        h->gseq = h->gseq % ((1u << 26) - 1) + 1;
-        HCHK(h, lpk::launch_group(h->ssel, A, par, cnt, chained ? 1 : 0, h->gseq, B, 1));
+        CALL(launch_group_timed(h, h->ssel, A, par, cnt, chained ? 1 : 0, 1));
         CALL(pev_at(h, ne++, &esel));
         HCHK(h, hipEventRecord(esel, h->ssel));
         last_sel = esel;
@@ -843,8 +871,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             // one persistent selection launch + one in-place sweep per group
             for (int64_t k = 0; k < b; k += B) {
                 const int cnt = (int)std::min<int64_t>(B, b - k);
-                h->gseq = h->gseq % ((1u << 26) - 1) + 1;
-                HCHK(h, lpk::launch_group(h->s, A[0], grp, cnt, chained ? 1 : 0, h->gseq, B, 0));
+                CALL(launch_group_timed(h, h->s, A[0], grp, cnt, chained ? 1 : 0, 0));
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
                 chained = true;
@@ -970,8 +997,17 @@ extern "C" int lp_profile(lp_handle *h, int enable)
         x->prof = enable != 0;
         x->prof_ms = 0.0;
         x->prof_n = 0;
+        x->sel_ms = 0.0;
+        x->sel_n = 0;
         x->evused = 0;
     }
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_select_time(lp_handle *h, double *ms, int64_t *launches)
+{
+    *ms = h->sel_ms;
+    *launches = h->sel_n;
     return LP_PIVOTED;
 }
 

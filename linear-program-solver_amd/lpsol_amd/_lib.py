@@ -71,6 +71,7 @@ _PROTOS = {
     "lp_get_block": (C.c_int, [_H, C.POINTER(C.c_int)]),
     "lp_profile": (C.c_int, [_H, C.c_int]),
     "lp_update_time": (C.c_int, [_H, _PD, _P64]),
+    "lp_select_time": (C.c_int, [_H, _PD, _P64]),
     "lp_last_error": (C.c_char_p, [_H]),
 }
 
@@ -268,6 +269,12 @@ class Engine:
         """-> (total ms, launches) of the rank-1 update kernel since profile()."""
         ms, n = C.c_double(), C.c_int64()
         self.lib.lp_update_time(self.h, C.byref(ms), C.byref(n))
+        return ms.value, n.value
+
+    def select_time(self):
+        """-> (total ms, launches) of the pivot-selection kernel since profile()."""
+        ms, n = C.c_double(), C.c_int64()
+        self.lib.lp_select_time(self.h, C.byref(ms), C.byref(n))
         return ms.value, n.value
 
 
