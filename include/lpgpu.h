@@ -73,7 +73,9 @@ int lp_create(int64_t m, int64_t n, int device, lp_handle **out);
 /* Row-sharded tableau for one rank of an nranks-process job (one GPU per
  * process).  Constraint rows are split in contiguous blocks; row 0 (the
  * objective) is replicated on every rank.  uid is the 128-byte RCCL unique id
- * from lp_comm_unique_id on rank 0, broadcast to all ranks by the caller. */
+ * from lp_comm_unique_id on rank 0, broadcast to all ranks by the caller;
+ * uid NULL creates no RCCL communicator (the device-side peer exchange below
+ * must then be set up: the per-pivot RCCL path is unavailable). */
 int lp_comm_unique_id(void *uid128);
 int lp_create_sharded(int64_t m, int64_t n, int device, int rank, int nranks,
                       const void *uid128, lp_handle **out);
@@ -85,6 +87,23 @@ int lp_create_sharded(int64_t m, int64_t n, int device, int rank, int nranks,
 int lp_create_group(int64_t m, int64_t n, int device, int nshards, lp_handle **out);
 /* This rank's constraint-row block [*row_begin, *row_begin + *row_count). */
 int lp_shard_rows(const lp_handle *h, int64_t *row_begin, int64_t *row_count);
+
+/* Device-side exchange between the ranks of a sharded job (one GPU per
+ * rank): the pivot selection runs as one persistent kernel per rank and
+ * group of pivots, exchanging the leaving-row candidates and the pivot row
+ * through the ranks' exchange buffers (peer stores over xGMI) instead of one
+ * RCCL collective per pivot.  Setup is collective:
+ *   lp_peer_handle  -> this rank's exchange-buffer IPC handle (LP_PEER_HANDLE_BYTES)
+ *   (the caller all-gathers the handles in rank order)
+ *   lp_peer_open    -> opens the peers' buffers and checks the exchange with
+ *                      a ping between all ranks; LP_DEVICE_ERROR if it fails
+ * If any rank fails, every rank calls lp_peer_enable(h, 0): the RCCL
+ * per-pivot path stays in use (identical results).  In-process shard groups
+ * (lp_create_group) set this up themselves. */
+#define LP_PEER_HANDLE_BYTES 64
+int lp_peer_handle(lp_handle *h, void *handle);
+int lp_peer_open(lp_handle *h, const void *handles);
+int lp_peer_enable(lp_handle *h, int enable);
 
 int lp_destroy(lp_handle *h);
 

@@ -129,8 +129,20 @@ struct Args {
     const double *Mp;    // previous group's M
     const long long *dRp;// previous group's local pivot rows
     int lag;
-    int pad2;
+    int rank;            // this rank (row-sharded jobs)
+    // row-sharded persistent selection: this rank's exchange buffer and every
+    // rank's (peer[rank] == xbuf), written by the peers over xGMI
+    unsigned long long *xbuf;
+    unsigned long long *const *peer;
 };
+
+// exchange buffer layout (granules of 8 bytes), see kernels.hip (XR)
+constexpr int NRANK_MAX = 64;
+constexpr long long XS_SUM_PAR = (NRANK_MAX + 1) * 8;            // per parity
+constexpr long long XS_PROW = 2 * XS_SUM_PAR;
+constexpr long long XS_PROW_BLOCK = 2 * 4 * 64;                   // 2 granules x 4 columns x 64 lanes
+constexpr long long XS_LOC = XS_PROW + 256 * XS_PROW_BLOCK;       // GROUP_MAXBLOCKS blocks
+constexpr long long XS_GRANULES = XS_LOC + 256 * 8;
 
 // launch wrappers (kernels.hip).  t = index of the pivot within its group
 // (known to the host, which enqueues the groups); grp = group parity.
@@ -146,10 +158,16 @@ hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, i
 // T_out <- A.T with the group's pivots (T_out == A.T: in place); nd_max >= ndef
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out);
 // one persistent launch selecting up to `count` chained pivots of a group;
-// seq numbers the launches of a handle (1 .. 2^26-1, then wraps to 1): it tags
+// seq numbers the launches of a handle (1 .. 2^24-1, then wraps to 1): it tags
 // the launch's summaries so no stale granule can match
+// xr: one rank of a row-sharded job.  As (device array of nshard Args): the
+// in-process shards of one device, all in this one launch
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax, int lag_layout);
+                        unsigned seq, int bmax, int lag_layout, int xr = 0,
+                        const Args *As = nullptr, int nshard = 1);
+// row-sharded: every rank writes a tagged granule to every rank's buffer and
+// waits (bounded) for all of them; *ok = 1 if all arrived (peer exchange works)
+hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, int *ok_dev);
 #ifndef LPK_GROUP_BLOCKS
 #define LPK_GROUP_BLOCKS 64
 #endif

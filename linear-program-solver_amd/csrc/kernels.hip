@@ -740,10 +740,12 @@ __device__ __forceinline__ double mk_d(unsigned lo, unsigned hi)
 __device__ __forceinline__ unsigned idx32(long long i) { return i == NONE ? 0x7fffffffu : (unsigned)i; }
 __device__ __forceinline__ long long un_idx(unsigned w) { return w == 0x7fffffffu ? NONE : (long long)w; }
 
-// the summary of pivot t, phase ph (0 ratio, 1 row 0) of launch seq
+// the summary of pivot t, phase ph of launch seq: 0 ratio, 1 row 0 (this
+// device); XR: 2 rank summary, 3 pivot-row slice, 4 / 5 straddle rescan;
+// 7 is the setup ping (never a pivot's tag)
 __device__ __forceinline__ unsigned gtag(unsigned seq, int t, int ph)
 {
-    return seq * (2 * BMAX) + 2 * t + ph;
+    return seq * (8 * BMAX) + 8 * t + ph;     // seq < 2^24 (the host wraps it)
 }
 
 // lanes 0..n-1 store word[lane] of this block's summary (after the drain)
@@ -787,6 +789,26 @@ __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[
     }
 }
 
+// lane f's value (f uniform)
+__device__ __forceinline__ unsigned rl32(unsigned v, int f) { return __builtin_amdgcn_readlane(v, f); }
+__device__ __forceinline__ double rl_d(unsigned lo, unsigned hi, int f)
+{
+    return mk_d(rl32(lo, f), rl32(hi, f));
+}
+
+// first summary (b = lane + 64k order) with l <= thr: returns k * 64 + lane, or -1
+template <int NR>
+__device__ __forceinline__ int first_in_band(const double (&l)[NR], unsigned G, double thr)
+{
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const unsigned b = threadIdx.x + k * GROUP_THREADS;
+        const u64 mask = __ballot(b < G && l[k] <= thr);
+        if (mask) return k * GROUP_THREADS + __builtin_ctzll(mask);
+    }
+    return -1;
+}
+
 // combine of G per-block summaries held in registers (summary b = lane + 64k):
 // two-pass semantics of the oracle.  The first summary inside the band is the
 // lowest lane of the first k whose ballot is non-empty.  Returns the winning
@@ -815,11 +837,64 @@ __device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[
 
 constexpr int CH = 8;    // deferred pivots applied per chunk (loads issued together)
 
-// NR = summaries per lane (G <= 64 NR); IPL = own columns per lane (cpb <= 64 IPL)
-template <int NR, int IPL>
-__global__ void __launch_bounds__(GROUP_THREADS)
-k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
+// ---- row-sharded persistent selection (XR): device-side exchange between
+// ranks through each rank's exchange buffer (xbuf), written by its peers over
+// xGMI with system-scope stores and polled locally (tagged 8-byte granules,
+// as inside a device).  Layout in granules:
+//   [XS_SUM]   2 parities x (NRANK_MAX + 1) slots x 8: the ranks' leaving-row
+//              summaries (slot NRANK_MAX: a straddle resolution)
+//   [XS_PROW]  GROUP_MAXBLOCKS x 512: the winning rank's pivot row, block b's
+//              columns as {lo, tag}, {hi, tag} granule pairs
+//   [XS_LOC]   GROUP_MAXBLOCKS x 8: this rank's per-block straddle rescans
+template <typename T>
+__device__ __forceinline__ void st_sys(T *p, T v)
 {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T ld_sys(const T *p)
+{
+    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// wall-clock bound of a cross-rank wait (the ranks' launches are enqueued by
+// different processes): 30 s of the 100 MHz real-time counter
+constexpr unsigned long long XWAIT_TICKS = 3000000000ull;
+
+// NG granules of each of n slots (slot p = lane p, p < n <= 64) at stride 8
+template <int NG>
+__device__ bool gather_x(const u64 *slots, int n, unsigned tag, unsigned (&w)[NG],
+                         unsigned *timeout_flag)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const int p = min((int)threadIdx.x, n - 1);
+    for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const u64 v = ld_sys(&slots[p * 8 + g]);
+            w[g] = (unsigned)v;
+            ok = ok && (unsigned)(v >> 32) == tag;
+        }
+        if (__all(ok)) return true;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+            st_sc1(timeout_flag, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// NR = summaries per lane (G <= 64 NR); IPL = own columns per lane (cpb <= 64 IPL);
+// XR = one rank of a row-sharded job (leaving row and pivot row exchanged
+// between ranks through the peers' exchange buffers)
+template <int NR, int IPL, bool XR>
+__global__ void __launch_bounds__(GROUP_THREADS)
+k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, unsigned seq, int bmax)
+{
+    // As: in-process shards of one device in ONE launch (gper blocks each, so
+    // every shard's blocks are co-resident); otherwise this device's A0
+    const Args A = As ? As[blockIdx.x / gper] : A0;
+    constexpr int NGRX = XR ? 7 : NGR;   // XR: the candidate's pivot element too
     __shared__ double sd[16];
     __shared__ long long sl[16];
     __shared__ long long sR[BMAX + CH];     // local pivot rows of this group
@@ -837,7 +912,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
     // blocks and the sweep.
     extern __shared__ __attribute__((aligned(16))) double dyn[];
     Ctl *ctl = A.ctl;
-    const unsigned G = gridDim.x, b = blockIdx.x;
+    const unsigned G = gper, b = blockIdx.x % gper;
     const int tid = threadIdx.x;
     constexpr int nth = GROUP_THREADS;
     // this parity's previous sweep is complete (the host orders it); the
@@ -1031,7 +1106,7 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
         const double lb = block_min(own && okown ? qown : INFINITY, sd);
         stamp(A, t, 4);
         long long ib = NONE;
-        double qb = 0.0;
+        double qb = 0.0, ab = 0.0;
         if (lb < INFINITY) {
             // own rows are lanes in row order: the first row inside the band
             // is the lowest lane that has one
@@ -1039,7 +1114,8 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
             const u64 mask = __ballot(own && okown && qown <= thr);
             const int f = __builtin_ctzll(mask);
             ib = lr0 + f;
-            qb = mk_d(__builtin_amdgcn_readlane(lo32(qown), f), __builtin_amdgcn_readlane(hi32(qown), f));
+            qb = rl_d(lo32(qown), hi32(qown), f);
+            if constexpr (XR) ab = rl_d(lo32(a), hi32(a), f);
         }
         {
             unsigned wv = idx32(ib);
@@ -1047,103 +1123,262 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
             else if (tid == 1) wv = hi32(lb);
             else if (tid == 2) wv = lo32(qb);
             else if (tid == 3) wv = hi32(qb);
-            publish(&grR[b * 8], gtag(seq, t, 0), wv, NGR);
+            else if (tid == 5) wv = lo32(ab);
+            else if (tid == 6) wv = hi32(ab);
+            publish(&grR[b * 8], gtag(seq, t, 0), wv, NGRX);
         }
         bstamp(A, t, 0);
         stamp(A, t, 5);
 
         // ---- leaving row (combine the ratio summaries)
-        double rl[NR], rq[NR];
-        long long ri[NR];
+        double rl[NR];
         double rmin = INFINITY;
-        {
-            unsigned w[NR][NGR];
-            if (!gather<NR, NGR>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout)) {
-                status = LP_DEVICE_ERROR;
-                break;
-            }
+        unsigned w[NR][NGRX];
+        if (!gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout)) {
+            status = LP_DEVICE_ERROR;
+            break;
+        }
 #pragma unroll
-            for (int k = 0; k < NR; ++k) {
-                const unsigned bb = tid + k * nth;
-                rl[k] = INFINITY;
-                rq[k] = 0.0;
-                ri[k] = NONE;
-                if (bb < G) {
-                    rl[k] = mk_d(w[k][0], w[k][1]);
-                    rq[k] = mk_d(w[k][2], w[k][3]);
-                    ri[k] = un_idx(w[k][4]);
-                    rmin = fmin(rmin, rl[k]);
-                }
+        for (int k = 0; k < NR; ++k) {
+            const unsigned bb = tid + k * nth;
+            rl[k] = INFINITY;
+            if (bb < G) {
+                rl[k] = mk_d(w[k][0], w[k][1]);
+                rmin = fmin(rmin, rl[k]);
             }
         }
         stamp(A, t, 6);
         const double g = block_min(rmin, sd);
-        if (!(g < INFINITY)) { status = LP_UNBOUNDED; break; }
-        const double thr = tie_band(g, A.tol.ratio_tie);
-        long long R = combine_loaded(rl, ri, rq, G, thr);
-        if (R < 0) {   // rare: rescan the selected block's rows (their M[t], col0 are published)
-            const long long bsel = -1 - R;
-            const long long r0 = 1 + bsel * rpb, r1 = min(r0 + rpb, A.rows);
-            long long mine = NONE;
-            for (long long lj = r0 + tid; lj < r1; lj += nth) {
-                bool ok;
-                const double q = row_ratio(ld_sc1(&A.M[mi(A.rows, lj, t)]), ld_sc1(&A.col0[lj]), A.tol, ok);
-                if (ok && q <= thr) { mine = lj; break; }
+        long long R = NONE;           // local row: this device's leaving row / candidate
+        double qR = 0.0, aR = 0.0;    // its ratio and pivot element (XR)
+        if (g < INFINITY) {
+            const double thr = tie_band(g, A.tol.ratio_tie);
+            const int bs = first_in_band(rl, G, thr);
+            const int k = bs / nth, f = bs % nth;
+            double q = 0.0, av_ = 0.0;
+            unsigned wi = 0;
+#pragma unroll
+            for (int kk = 0; kk < NR; ++kk)
+                if (kk == k) {
+                    q = rl_d(w[kk][2], w[kk][3], f);
+                    wi = rl32(w[kk][4], f);
+                    if constexpr (XR) av_ = rl_d(w[kk][5], w[kk][6], f);
+                }
+            if (q <= thr) {
+                R = un_idx(wi);
+                qR = q;
+                aR = av_;
+            } else {   // rare: rescan the selected block's rows (their M[t], col0 are published)
+                const long long r0 = 1 + (long long)bs * rpb, r1 = min(r0 + rpb, A.rows);
+                long long mine = NONE;
+                double qm = 0.0, am = 0.0;
+                for (long long lj = r0 + tid; lj < r1; lj += nth) {
+                    bool ok;
+                    const double mv = ld_sc1(&A.M[mi(A.rows, lj, t)]);
+                    const double qq = row_ratio(mv, ld_sc1(&A.col0[lj]), A.tol, ok);
+                    if (ok && qq <= thr) { mine = lj; qm = qq; am = mv; break; }
+                }
+                R = block_min_ll(mine, sl);
+                const int fr = __builtin_ctzll(__ballot(mine == R));
+                qR = rl_d(lo32(qm), hi32(qm), fr);
+                aR = rl_d(lo32(am), hi32(am), fr);
             }
-            R = block_min_ll(mine, sl);
+        } else if (!XR) {
+            status = LP_UNBOUNDED;
+            break;
+        }
+        bool win = true;              // this rank holds the leaving row
+        long long rglob = R - 1 + A.rb;
+        if constexpr (XR) {
+            // ---- leaving row across ranks: every rank sends (local minimum,
+            //      candidate's ratio, global row, pivot element) to all ranks
+            const int par = t & 1;
+            const int N = A.nranks;
+            u64 *xs = A.xbuf + par * XS_SUM_PAR;           // local slots, written by the peers
+            if (b == 0 && tid < 7) {
+                const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
+                unsigned wv = 0;
+                if (tid == 0) wv = lo32(g);
+                else if (tid == 1) wv = hi32(g);
+                else if (tid == 2) wv = lo32(qR);
+                else if (tid == 3) wv = hi32(qR);
+                else if (tid == 4) wv = R == NONE ? 0xffffffffu : (unsigned)rglob;
+                else if (tid == 5) wv = lo32(aR);
+                else wv = hi32(aR);
+                for (int p = 0; p < N; ++p)
+                    st_sys(&A.peer[p][par * XS_SUM_PAR + A.rank * 8 + tid], tg | wv);
+            }
+            unsigned x[7];
+            if (!gather_x<7>(xs, N, gtag(seq, t, 2), x, &ctl->bar_timeout)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
+            const double lp = (int)tid < N ? mk_d(x[0], x[1]) : INFINITY;
+            const double gg = wave_min(lp);
+            if (!(gg < INFINITY)) { status = LP_UNBOUNDED; break; }
+            const double thr = tie_band(gg, A.tol.ratio_tie);
+            const int ps = __builtin_ctzll(__ballot((int)tid < N && lp <= thr));
+            const double qs = rl_d(x[2], x[3], ps);
+            long long rg;
+            double as;
+            if (qs <= thr) {
+                rg = (long long)rl32(x[4], ps);
+                as = rl_d(x[5], x[6], ps);
+            } else {
+                // rare: a near-tie straddles the band across ranks.  Rank ps
+                // (the first with a row inside it) finds its first such row:
+                // each block offers its first own row, block 0 sends the lowest
+                // to every rank (the straddle slot)
+                if (A.rank == ps) {
+                    const u64 mk = __ballot(own && okown && qown <= thr);
+                    const int fr = mk ? __builtin_ctzll(mk) : 0;
+                    const long long ir = mk ? lr0 + fr : NONE;
+                    const double ar = rl_d(lo32(a), hi32(a), fr);
+                    u64 *loc = A.xbuf + XS_LOC;
+                    if (tid < 3) {
+                        const unsigned wv = tid == 0 ? idx32(ir) : tid == 1 ? lo32(ar) : hi32(ar);
+                        st_sc1(&loc[b * 8 + tid], ((u64)gtag(seq, t, 4) << 32) | wv);
+                    }
+                    unsigned wl[NR][3];
+                    if (!gather<NR, 3>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout)) {
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    double il[NR];
+#pragma unroll
+                    for (int k = 0; k < NR; ++k)
+                        il[k] = (tid + k * nth < G && wl[k][0] != 0x7fffffffu) ? 0.0 : INFINITY;
+                    const int bf = first_in_band(il, G, 0.0);
+                    const int kf = bf / nth, ff = bf % nth;
+                    unsigned r0w = 0, a0 = 0, a1 = 0;
+#pragma unroll
+                    for (int kk = 0; kk < NR; ++kk)
+                        if (kk == kf) {
+                            r0w = rl32(wl[kk][0], ff);
+                            a0 = rl32(wl[kk][1], ff);
+                            a1 = rl32(wl[kk][2], ff);
+                        }
+                    if (b == 0 && tid < 3) {
+                        const unsigned wv = tid == 0 ? (unsigned)((long long)r0w - 1 + A.rb) : tid == 1 ? a0 : a1;
+                        for (int p = 0; p < N; ++p)
+                            st_sys(&A.peer[p][par * XS_SUM_PAR + NRANK_MAX * 8 + tid],
+                                   ((u64)gtag(seq, t, 5) << 32) | wv);
+                    }
+                }
+                unsigned y[3];
+                if (!gather_x<3>(xs + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctl->bar_timeout)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                rg = (long long)__builtin_amdgcn_readfirstlane(y[0]);
+                as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
+            }
+            win = A.rank == ps;
+            rglob = rg;
+            R = win ? rg - A.rb + 1 : -1;
+            aR = as;
         }
         if (li == R) ownpiv |= 1ull << t;
         stamp(A, t, 7);
         // ---- pivot row on own columns, row 0 on own columns.  Tableau row
         //      loads first, then the cross-block loads (one round trip).
-        double xv[IPL];
-#pragma unroll
-        for (int k = 0; k < IPL; ++k) {
-            const long long j = jc0 + tid + k * nth;
-            xv[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
-        }
-        if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, R, tid)]);
-        if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, R, tid)];
-        if (tid == 0) sR[t] = R;
+        double pv_[IPL];                  // this pivot's normalised row on own columns
         const double f0 = ld_sc1(&A.M[mi(A.rows, 0, t)]);
-        // pivots s whose pivot row is R: the select instead of the FMA (uniform)
-        const u64 rpiv = __ballot(tid < t && sR[tid] == R);
-        const u64 rpivp = __ballot(tid < np && sRp[tid] == R);
-        __syncthreads();
-        stamp(A, t, 8);
-        const double av = sMr[t];
-        // deferred pivots of the previous group (lag), then 0..t-1 of this
-        // group, on the own columns, CH at a time
-        auto chain_row = [&](int nt, const double *smr, const double *const (&pc)[IPL], u64 piv) {
-            for (int s0 = 0; s0 < nt; s0 += CH) {
-                double mr[CH], pv[CH][IPL];
+        if (win) {
+            double xv[IPL];
 #pragma unroll
-                for (int u = 0; u < CH; ++u) {
-                    mr[u] = smr[s0 + u];
+            for (int k = 0; k < IPL; ++k) {
+                const long long j = jc0 + tid + k * nth;
+                xv[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
+            }
+            if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, R, tid)]);
+            if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, R, tid)];
+            if (tid == 0) sR[t] = R;
+            // pivots s whose pivot row is R: the select instead of the FMA (uniform)
+            const u64 rpiv = __ballot(tid < t && sR[tid] == R);
+            const u64 rpivp = __ballot(tid < np && sRp[tid] == R);
+            __syncthreads();
+            stamp(A, t, 8);
+            const double av = XR ? aR : sMr[t];
+            // deferred pivots of the previous group (lag), then 0..t-1 of this
+            // group, on the own columns, CH at a time
+            auto chain_row = [&](int nt, const double *smr, const double *const (&pc)[IPL], u64 piv) {
+                for (int s0 = 0; s0 < nt; s0 += CH) {
+                    double mr[CH], pv[CH][IPL];
 #pragma unroll
-                    for (int k = 0; k < IPL; ++k) pv[u][k] = pc[k][s0 + u];
+                    for (int u = 0; u < CH; ++u) {
+                        mr[u] = smr[s0 + u];
+#pragma unroll
+                        for (int k = 0; k < IPL; ++k) pv[u][k] = pc[k][s0 + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < CH; ++u)
+                        if (s0 + u < nt) {
+                            if ((piv >> (s0 + u)) & 1) {     // row R was pivot row s
+#pragma unroll
+                                for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
+                            } else {
+#pragma unroll
+                                for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
+                            }
+                        }
                 }
+            };
+            chain_row(np, sMrp, pcolp, rpivp);
+            chain_row(t, sMr, pcol, rpiv);
 #pragma unroll
-                for (int u = 0; u < CH; ++u)
-                    if (s0 + u < nt) {
-                        if ((piv >> (s0 + u)) & 1) {     // row R was pivot row s
+            for (int k = 0; k < IPL; ++k) {
+                const long long j = jc0 + tid + k * nth;
+                pv_[k] = (j == C) ? 1.0 : xv[k] / av;
+            }
+            if constexpr (XR) {
+                // the other ranks' block b gets this block's columns
+                const unsigned long long tg = (u64)gtag(seq, t, 3) << 32;
+                for (int p = 0; p < A.nranks; ++p) {
+                    if (p == A.rank) continue;
+                    u64 *dst = A.peer[p] + XS_PROW + (long long)b * XS_PROW_BLOCK;
 #pragma unroll
-                            for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
-                        } else {
-#pragma unroll
-                            for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
+                    for (int k = 0; k < IPL; ++k) {
+                        const int kk = tid + k * nth;
+                        if (jc0 + kk < jc1) {
+                            st_sys(&dst[2 * kk], tg | lo32(pv_[k]));
+                            st_sys(&dst[2 * kk + 1], tg | hi32(pv_[k]));
                         }
                     }
+                }
             }
-        };
-        chain_row(np, sMrp, pcolp, rpivp);
-        chain_row(t, sMr, pcol, rpiv);
+        } else if constexpr (XR) {
+            if (tid == 0) sR[t] = -1;
+            // the winning rank's block b sends these columns
+            const u64 *src = A.xbuf + XS_PROW + (long long)b * XS_PROW_BLOCK;
+            const unsigned tg = gtag(seq, t, 3);
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int k = 0; k < IPL; ++k) {
+                    const int kk = min((long long)tid + k * nth, cpb - 1);
+                    const u64 lo = ld_sys(&src[2 * kk]), hi = ld_sys(&src[2 * kk + 1]);
+                    pv_[k] = mk_d((unsigned)lo, (unsigned)hi);
+                    ok = ok && (jc0 + kk >= jc1 || ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
+                }
+                if (__all(ok)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+                    st_sc1(&ctl->bar_timeout, 1u);
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (status != LP_PIVOTED) break;
+            __syncthreads();
+        }
         double vmin = INFINITY, v0 = 0.0;
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             const long long j = jc0 + tid + k * nth;
             if (j < jc1) {
-                const double p = (j == C) ? 1.0 : xv[k] / av;
+                const double p = pv_[k];
                 lP[kc[k] * cs + t] = p;
                 st_sc1(&A.P[t * A.ld + j], p);
                 const double v = upd(0, -1, f0, p, l0[kc[k]]);
@@ -1184,7 +1419,6 @@ k_group(Args A, int grp, int count, int from_erec, unsigned seq, int bmax)
         }
         stamp(A, t, 10);
         if (b == 0 && tid == 0) {     // column 0 is in block 0's slice: v0 = new row0[0]
-            const long long rglob = R - 1 + A.rb;
             st_sc1(&A.dR[t], R);
             st_sc1(&A.dC[t], C);
             st_sc1(&ctl->r, rglob);
@@ -1347,6 +1581,25 @@ k_sweep(const double *T, double *Tout, const double *__restrict__ P,
         if (k < nr) *reinterpret_cast<double2 *>(Tout + (rb + k) * ld + j0) = x[k];
 }
 
+// peer exchange check (row-sharded setup): lane p writes this rank's granule
+// into rank p's summary slot, then every lane waits for rank p's granule in
+// the local buffer (bounded)
+__global__ void k_peer_ping(Args A, unsigned tag, int *ok)
+{
+    const int N = A.nranks, p = threadIdx.x;
+    if (p < N) st_sys(&A.peer[p][A.rank * 8], ((u64)tag << 32) | (unsigned)A.rank);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool got = p >= N;
+    while (!got) {
+        const u64 v = ld_sys(&A.xbuf[p * 8]);
+        got = (unsigned)(v >> 32) == tag && (unsigned)v == (unsigned)p;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;   // 2 s
+        __builtin_amdgcn_s_sleep(2);
+    }
+    const bool all = __all(got);
+    if (threadIdx.x == 0) *ok = all ? 1 : 0;
+}
+
 __global__ void k_resume(Ctl *ctl)
 {
     ctl->status = LP_PIVOTED;
@@ -1462,19 +1715,30 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 }
 
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax, int lag_layout)
+                        unsigned seq, int bmax, int lag_layout, int xr, const Args *As, int nshard)
 {
+    if (xr && (lag_layout || A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
     if (count < 1 || count > bmax || bmax > BMAX || (A.lag && !lag_layout)) return hipErrorInvalidValue;
     // every launch of a chain must have the same geometry (the next one reads
     // the plain per-block summaries this one leaves): sized by lag_layout
-    const long long g = group_blocks(A.rc, A.ld, bmax, lag_layout);
+    // a sharded job: every rank the same geometry (the column slices of block b
+    // must match across ranks), sized for the largest row block
+    const long long rcg = xr ? (A.m + A.nranks - 1) / A.nranks : A.rc;
+    const long long g = group_blocks(rcg, A.ld, bmax, lag_layout);
     if (g == 0) return hipErrorInvalidValue;
-    const size_t lds = (size_t)group_lds(A.rc, A.ld, g, bmax, lag_layout);
+    const size_t lds = (size_t)group_lds(rcg, A.ld, g, bmax, lag_layout);
     const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
     const int ipl = (int)(((A.ld + g - 1) / g + GROUP_THREADS - 1) / GROUP_THREADS);
+    const dim3 grid((unsigned)(g * (As ? nshard : 1)));
 #define GROUP_LAUNCH(NRV, IPLV)                                                               \
-    hipLaunchKernelGGL((k_group<NRV, IPLV>), dim3((unsigned)g), dim3(GROUP_THREADS), lds, s,  \
-                       A, grp, count, from_erec, seq, bmax)
+    do {                                                                                      \
+        if (xr)                                                                               \
+            hipLaunchKernelGGL((k_group<NRV, IPLV, true>), grid, dim3(GROUP_THREADS), lds, s, \
+                               A, As, (int)g, grp, count, from_erec, seq, bmax);              \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_group<NRV, IPLV, false>), grid, dim3(GROUP_THREADS), lds, s, \
+                               A, As, (int)g, grp, count, from_erec, seq, bmax);              \
+    } while (0)
     if (ipl <= 2) {
         if (nr <= 1) GROUP_LAUNCH(1, 2);
         else if (nr <= 2) GROUP_LAUNCH(2, 2);
@@ -1491,6 +1755,13 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
 hipError_t launch_resume(hipStream_t s, const Args &A)
 {
     hipLaunchKernelGGL(k_resume, dim3(1), dim3(1), 0, s, A.ctl);
+    return hipGetLastError();
+}
+
+hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, int *ok_dev)
+{
+    if (A.nranks > NRANK_MAX || !A.xbuf || !A.peer) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_peer_ping, dim3(1), dim3(64), 0, s, A, tag, ok_dev);
     return hipGetLastError();
 }
 

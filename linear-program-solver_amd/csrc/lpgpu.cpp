@@ -52,7 +52,15 @@ struct lp_handle {
     double *T2 = nullptr;           // second tableau buffer
     hipStream_t ssel = nullptr, ssw = nullptr;   // CU-partitioned streams
     int sel_cus = 0;                // CUs of the selection stream
+    size_t pev_used = 0;            // events of pev handed out since the last sync
     std::vector<hipEvent_t> pev;    // ordering events, reused per batch
+    // row-sharded persistent selection: device-side exchange between ranks
+    unsigned long long *xbuf = nullptr;     // this rank's exchange buffer (peers write it)
+    unsigned long long **dpeer = nullptr;   // device table: every rank's buffer
+    std::vector<void *> ipc_open;           // peer buffers opened from IPC handles
+    bool peer_ok = false;                   // the exchange is set up and validated
+    bool peer_enable = true;                // LPGPU_PEER=0 keeps the RCCL per-pivot path
+    hipStream_t sx = nullptr;               // in-process shards: own stream for the persistent launch
     bool eager_ok = false;          // row0/col0 mirror the stored tableau
     Ctl *ctl = nullptr;
     Ctl *hctl = nullptr;            // pinned mirror
@@ -123,7 +131,7 @@ struct Comm {
 };
 
 struct RcclComm : Comm {
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;      // null: peer exchange only (no RCCL communicator)
     ~RcclComm() override
     {
         if (comm) ncclCommDestroy(comm);
@@ -132,12 +140,14 @@ struct RcclComm : Comm {
     int allreduce_min(const Members &M) override
     {
         lp_handle *h = M[0];
+        if (!comm) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator (created without a unique id)");
         NCHK(h, ncclAllReduce(h->xg, h->xg, 1, ncclFloat64, ncclMin, comm, h->s));
         return LP_PIVOTED;
     }
     int allgather(const Members &M) override
     {
         lp_handle *h = M[0];
+        if (!comm) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator (created without a unique id)");
         NCHK(h, ncclAllGather(h->xs, h->xr, (size_t)slot_len(h), ncclFloat64, comm, h->s));
         return LP_PIVOTED;
     }
@@ -146,11 +156,22 @@ struct RcclComm : Comm {
 struct GroupComm : Comm {
     Members all;                   // every shard, rank order
     double **dptrs = nullptr;      // device array of the shards' xg pointers
+    Args *dargs = nullptr;         // device array of the shards' kernel arguments
+    std::vector<Args> hargs;       // pinned-free staging copy (kept alive until the next sync)
     hipStream_t s = nullptr;       // shared by all shards, released with the last one
     ~GroupComm() override
     {
         if (dptrs) (void)hipFree(dptrs);
+        if (dargs) (void)hipFree(dargs);
         if (s) (void)hipStreamDestroy(s);
+    }
+    // the shards' arguments for a one-launch persistent selection
+    int stage_args(lp_handle *h, const std::vector<Args> &A)
+    {
+        if (!dargs) HCHK(h, hipMalloc(&dargs, all.size() * sizeof(Args)));
+        hargs = A;
+        HCHK(h, hipMemcpyAsync(dargs, hargs.data(), A.size() * sizeof(Args), hipMemcpyHostToDevice, s));
+        return LP_PIVOTED;
     }
     Members members(lp_handle *) override { return all; }
     int allreduce_min(const Members &M) override
@@ -209,7 +230,9 @@ static Args args_of(const lp_handle *h)
     A.Mp = nullptr;
     A.dRp = nullptr;
     A.lag = 0;
-    A.pad2 = 0;
+    A.rank = h->rank;
+    A.xbuf = h->xbuf;
+    A.peer = h->dpeer;
     return A;
 }
 
@@ -267,6 +290,7 @@ static int alloc_handle(lp_handle *h)
     if (const char *sel = std::getenv("LPGPU_SELECT"))
         h->persistent = std::strcmp(sel, "kernels") != 0;
     if (const char *pl = std::getenv("LPGPU_PIPELINE")) h->pipeline = pl[0] == '1';
+    if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
     if (const char *sc = std::getenv("LPGPU_SEL_CUS")) h->sel_cus = std::atoi(sc);
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
@@ -364,7 +388,7 @@ extern "C" int lp_create_sharded(int64_t m, int64_t n, int device, int rank, int
     auto comm = std::make_shared<RcclComm>();
     h->comm = comm;
     int st = alloc_handle(h);
-    if (st == LP_PIVOTED) {
+    if (st == LP_PIVOTED && uid128) {
         ncclUniqueId id;
         std::memcpy(&id, uid128, sizeof(id));
         const ncclResult_t r = ncclCommInitRank(&comm->comm, nranks, id, rank);
@@ -411,6 +435,32 @@ extern "C" int lp_create_group(int64_t m, int64_t n, int device, int nshards, lp
         if (st != LP_PIVOTED) g_create_err = h->err;
     }
     if (st == LP_PIVOTED) {
+        // device-side exchange between the shards (same device: plain buffers)
+        std::vector<unsigned long long *> xb;
+        for (lp_handle *h : grp->all) {
+            if (!h->peer_enable || nshards > lpk::NRANK_MAX) break;
+            const size_t xbytes = lpk::XS_GRANULES * sizeof(unsigned long long);
+            if (hipMalloc(&h->xbuf, xbytes) != hipSuccess || hipMemset(h->xbuf, 0, xbytes) != hipSuccess ||
+                hipStreamCreateWithFlags(&h->sx, hipStreamNonBlocking) != hipSuccess) {
+                g_create_err = "group exchange buffers";
+                st = LP_DEVICE_ERROR;
+                break;
+            }
+            xb.push_back(h->xbuf);
+        }
+        if (st == LP_PIVOTED && xb.size() == grp->all.size())
+            for (lp_handle *h : grp->all) {
+                if (hipMalloc(&h->dpeer, xb.size() * sizeof(void *)) != hipSuccess ||
+                    hipMemcpy(h->dpeer, xb.data(), xb.size() * sizeof(void *), hipMemcpyHostToDevice) !=
+                        hipSuccess) {
+                    g_create_err = "group exchange table";
+                    st = LP_DEVICE_ERROR;
+                    break;
+                }
+                h->peer_ok = true;
+            }
+    }
+    if (st == LP_PIVOTED) {
         std::vector<double *> p;
         for (lp_handle *h : grp->all) p.push_back(h->xg);
         if (hipMalloc(&grp->dptrs, p.size() * sizeof(double *)) != hipSuccess ||
@@ -431,6 +481,82 @@ extern "C" int lp_create_group(int64_t m, int64_t n, int device, int nshards, lp
     return LP_PIVOTED;
 }
 
+// ---------------------------------------------------------------------------
+// device-side exchange between the ranks of a sharded job
+// ---------------------------------------------------------------------------
+
+extern "C" int lp_peer_handle(lp_handle *h, void *ipc64)
+{
+    if (!h || !h->comm || h->nranks > lpk::NRANK_MAX) return h ? fail(h, LP_BAD_ARG, "not a sharded handle") : LP_BAD_ARG;
+    HCHK(h, hipSetDevice(h->dev));
+    const size_t xbytes = lpk::XS_GRANULES * sizeof(unsigned long long);
+    hipIpcMemHandle_t hd;
+    if (!h->xbuf) {
+        // fine-grained: peers' system-scope stores are visible to this device's
+        // polling loads; plain device memory if that cannot be shared
+        if (hipExtMallocWithFlags((void **)&h->xbuf, xbytes, hipDeviceMallocFinegrained) != hipSuccess ||
+            hipIpcGetMemHandle(&hd, h->xbuf) != hipSuccess) {
+            if (h->xbuf) (void)hipFree(h->xbuf);
+            h->xbuf = nullptr;
+            (void)hipGetLastError();
+            HCHK(h, hipMalloc(&h->xbuf, xbytes));
+        }
+        HCHK(h, hipMemset(h->xbuf, 0, xbytes));
+    }
+    HCHK(h, hipIpcGetMemHandle(&hd, h->xbuf));
+    static_assert(sizeof(hd) == LP_PEER_HANDLE_BYTES, "IPC handle size");
+    std::memcpy(ipc64, &hd, sizeof(hd));
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_peer_open(lp_handle *h, const void *handles)
+{
+    if (!h || !h->comm || !h->xbuf) return h ? fail(h, LP_BAD_ARG, "lp_peer_handle first") : LP_BAD_ARG;
+    HCHK(h, hipSetDevice(h->dev));
+    std::vector<unsigned long long *> tab(h->nranks, nullptr);
+    const char *all = static_cast<const char *>(handles);
+    for (int p = 0; p < h->nranks; ++p) {
+        if (p == h->rank) {
+            tab[p] = h->xbuf;
+            continue;
+        }
+        hipIpcMemHandle_t hd;
+        std::memcpy(&hd, all + (size_t)p * LP_PEER_HANDLE_BYTES, sizeof(hd));
+        void *ptr = nullptr;
+        HCHK(h, hipIpcOpenMemHandle(&ptr, hd, hipIpcMemLazyEnablePeerAccess));
+        h->ipc_open.push_back(ptr);
+        tab[p] = static_cast<unsigned long long *>(ptr);
+    }
+    if (!h->dpeer) HCHK(h, hipMalloc(&h->dpeer, lpk::NRANK_MAX * sizeof(void *)));
+    HCHK(h, hipMemcpy(h->dpeer, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice));
+    // every rank pings every rank (collective: all ranks call this together)
+    int *dok = nullptr, ok = 0;
+    HCHK(h, hipMalloc(&dok, sizeof(int)));
+    Args A = args_of(h);
+    A.peer = h->dpeer;
+    const hipError_t e = lpk::launch_peer_ping(h->s, A, 7u, dok);
+    if (e == hipSuccess) (void)hipMemcpyAsync(&ok, dok, sizeof(int), hipMemcpyDeviceToHost, h->s);
+    const hipError_t e2 = hipStreamSynchronize(h->s);
+    (void)hipFree(dok);
+    if (e != hipSuccess || e2 != hipSuccess) return fail(h, LP_DEVICE_ERROR, "peer ping launch failed");
+    // the ping used the summary slots: clear them for the pivots
+    HCHK(h, hipMemset(h->xbuf, 0, lpk::XS_GRANULES * sizeof(unsigned long long)));
+    HCHK(h, hipDeviceSynchronize());
+    if (!ok) return fail(h, LP_DEVICE_ERROR, "peer exchange check timed out");
+    h->peer_ok = true;
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_peer_enable(lp_handle *h, int enable)
+{
+    for (lp_handle *x : members_of(h))
+        if (x) {
+            if (enable && !x->dpeer) return fail(h, LP_BAD_ARG, "no peer exchange set up");
+            x->peer_ok = enable != 0;
+        }
+    return LP_PIVOTED;
+}
+
 extern "C" int lp_shard_rows(const lp_handle *h, int64_t *row_begin, int64_t *row_count)
 {
     *row_begin = h->rb;
@@ -444,6 +570,11 @@ extern "C" int lp_destroy(lp_handle *h)
     (void)hipSetDevice(h->dev);
     if (h->s) (void)hipStreamSynchronize(h->s);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
+    if (h->sx) (void)hipStreamSynchronize(h->sx);
+    for (void *p : h->ipc_open) (void)hipIpcCloseMemHandle(p);
+    if (h->dpeer) (void)hipFree(h->dpeer);
+    if (h->xbuf) (void)hipFree(h->xbuf);
+    if (h->sx) (void)hipStreamDestroy(h->sx);
     if (h->ssel) (void)hipStreamSynchronize(h->ssel);
     if (h->ssw) (void)hipStreamSynchronize(h->ssw);
     for (hipEvent_t e : h->pev) (void)hipEventDestroy(e);
@@ -622,12 +753,39 @@ static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, hipStream_t 
 }
 
 static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int grp, int cnt,
-                              int from_erec, int lag_layout)
+                              int from_erec, int lag_layout, int xr = 0,
+                              const Args *As = nullptr, int nshard = 1)
 {
-    h->gseq = h->gseq % ((1u << 26) - 1) + 1;
+    // every rank of a sharded job advances gseq identically (same calls, same order)
+    h->gseq = h->gseq % ((1u << 24) - 1) + 1;
     CALL(prof_begin(h, st));
-    HCHK(h, lpk::launch_group(st, A, grp, cnt, from_erec, h->gseq, h->block, lag_layout));
+    HCHK(h, lpk::launch_group(st, A, grp, cnt, from_erec, h->gseq, h->block, lag_layout, xr, As,
+                              nshard));
     return prof_end(h, st, 1);
+}
+
+static int pev_at(lp_handle *h, size_t k, hipEvent_t *e);
+
+// row-sharded persistent selection usable for this shape?
+static bool xr_ok(const lp_handle *h)
+{
+    if (!h->comm || !h->peer_ok || !h->persistent) return false;
+    const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
+    return lpk::group_blocks(rcmax, h->ld, h->block, 0) > 0;
+}
+
+// one persistent selection launch per rank for a group of cnt pivots.  The
+// in-process shards of one device go into ONE launch (their blocks wait on
+// each other, so all of them must be resident together).
+static int enqueue_xgroup(const Members &M, const std::vector<Args> &A, int grp, int cnt,
+                          int from_erec)
+{
+    if (M.size() == 1) return launch_group_timed(M[0], M[0]->s, A[0], grp, cnt, from_erec, 0, 1);
+    lp_handle *h0 = M[0];
+    auto g = std::dynamic_pointer_cast<GroupComm>(h0->comm);
+    if (!g) return fail(h0, LP_DEVICE_ERROR, "multi-member launch without a shard group");
+    CALL(g->stage_args(h0, A));
+    return launch_group_timed(h0, h0->s, A[0], grp, cnt, from_erec, 0, 1, g->dargs, (int)M.size());
 }
 
 // after a stream sync: fold recorded sweep launches into the totals
@@ -865,7 +1023,18 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
                                lpk::group_blocks(h->rc, h->ld, B, 1) > 0;
         int ngroups = 0;
         const int64_t before = done;
-        if (pipelined) {
+        h->pev_used = 0;
+        if (xr_ok(h)) {
+            // row-sharded: one persistent selection launch per rank and group,
+            // leaving row and pivot row exchanged device-side between ranks
+            for (int64_t k = 0; k < b; k += B) {
+                const int cnt = (int)std::min<int64_t>(B, b - k);
+                CALL(enqueue_xgroup(M, A, grp, cnt, chained ? 1 : 0));
+                CALL(enqueue_sweep(M, A, grp));
+                grp ^= 1;
+                chained = true;
+            }
+        } else if (pipelined) {
             CALL(enqueue_pipelined(h, b, chained, &ngroups));
         } else if (!h->comm && h->persistent && lpk::group_blocks(h->rc, h->ld, B, 0) > 0) {
             // one persistent selection launch + one in-place sweep per group

@@ -72,6 +72,9 @@ _PROTOS = {
     "lp_profile": (C.c_int, [_H, C.c_int]),
     "lp_update_time": (C.c_int, [_H, _PD, _P64]),
     "lp_select_time": (C.c_int, [_H, _PD, _P64]),
+    "lp_peer_handle": (C.c_int, [_H, C.c_char_p]),
+    "lp_peer_open": (C.c_int, [_H, C.c_char_p]),
+    "lp_peer_enable": (C.c_int, [_H, C.c_int]),
     "lp_last_error": (C.c_char_p, [_H]),
 }
 
@@ -271,6 +274,22 @@ class Engine:
         self.lib.lp_update_time(self.h, C.byref(ms), C.byref(n))
         return ms.value, n.value
 
+    # ---- device-side exchange between the ranks of a sharded job
+    PEER_HANDLE_BYTES = 64
+
+    def peer_handle(self) -> bytes:
+        """This rank's exchange-buffer IPC handle (all-gather it in rank order)."""
+        buf = C.create_string_buffer(self.PEER_HANDLE_BYTES)
+        self._check(self.lib.lp_peer_handle(self.h, buf), self.h)
+        return buf.raw
+
+    def peer_open(self, handles: bytes):
+        """Open every rank's buffer and check the exchange (collective)."""
+        self._check(self.lib.lp_peer_open(self.h, handles), self.h)
+
+    def peer_enable(self, enable: bool):
+        self._check(self.lib.lp_peer_enable(self.h, 1 if enable else 0), self.h)
+
     def select_time(self):
         """-> (total ms, launches) of the pivot-selection kernel since profile()."""
         ms, n = C.c_double(), C.c_int64()
@@ -309,8 +328,8 @@ def create_sharded(m: int, n: int, rank: int, nranks: int, uid: bytes,
     lib = load()
     if device_count() <= device:
         raise EngineUnavailable("no GPU visible; the engine has no CPU fallback")
-    if len(uid) != 128:
-        raise ValueError("uid must be the 128-byte RCCL unique id")
+    if uid is not None and len(uid) != 128:
+        raise ValueError("uid must be the 128-byte RCCL unique id (or None: no RCCL)")
     h = _H()
     st = lib.lp_create_sharded(m, n, device, rank, nranks, uid, C.byref(h))
     if st != PIVOTED:

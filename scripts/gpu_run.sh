@@ -31,8 +31,14 @@ for step in "$@"; do
                 run benchp_b$B 300 python bench.py --no-cpu-baseline --block $B
             done
             LPGPU_SELECT=kernels run benchk_b16 300 python bench.py --no-cpu-baseline --block 16 ;;
+        shards)
+            for S in 2 8; do
+                run bench_shards$S 600 python bench.py --no-cpu-baseline --group-shards $S --steps 256
+            done ;;
         cfg4one)
-            run bench_cfg4_1gpu 600 python bench.py --no-cpu-baseline --block 16 --emulate-ranks 8 --steps 256 ;;
+            for B in 16 32; do
+                run bench_cfg4_1gpu_b$B 600 python bench.py --no-cpu-baseline --block $B --emulate-ranks 8 --steps 256
+            done ;;
         dist2)
             run bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 64 --warmup 8 ;;
         prof16)
@@ -92,7 +98,7 @@ for step in "$@"; do
             export TMPDIR=/tmp
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
-            run pmc_json 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" --block 16
+            run pmc_json 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" --block 32
             # later steps of this call (bench) report it as roofline.traffic
             if [ -f "$OUT/hbm_traffic.json" ]; then cp "$OUT/hbm_traffic.json" profiles/r01/hbm_traffic.json; fi ;;
         proffinal)

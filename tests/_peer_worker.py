@@ -1,0 +1,47 @@
+"""One rank of a 2-process row-sharded job on ONE GPU (test_gpu_peer_procs.py):
+no RCCL communicator (RCCL refuses two ranks on one device); the device-side
+peer exchange is set up from IPC handles all-gathered over gloo."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
+sys.path.insert(0, ROOT)
+
+import torch.distributed as dist  # noqa: E402
+
+from lpsol_amd import _lib, generators as gen  # noqa: E402
+from oracle.f64 import F64Tableau  # noqa: E402
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    kind, m, ns, k, block, tie = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), \
+        int(sys.argv[5]), float(sys.argv[6])
+    T = gen.tableau(kind, m, ns, 31)
+    m, n = T.shape[0] - 1, T.shape[1] - 1
+    e = _lib.create_sharded(m, n, rank, world, None, device=0)
+    hs = [None] * world
+    dist.all_gather_object(hs, e.peer_handle())
+    e.peer_open(b"".join(hs))
+    e.upload(T)
+    e.set_block(block)
+    e.set_tol(ratio_tie=tie)
+    st, done = e.run(_lib.RULE_STANDARD, k)
+    o = F64Tableau(T, {"ratio_tie": tie})
+    ost, olog = o.run(0, k)
+    assert e.log().tolist() == olog.tolist(), (rank, e.log().tolist()[:5], olog.tolist()[:5])
+    b, c = e.row_begin, e.row_count
+    assert np.array_equal(e.rows(0, 1), o.T[:1])
+    assert np.array_equal(e.rows(1 + b, c), o.T[1 + b:1 + b + c])
+    dist.barrier()
+    e.close()
+    dist.destroy_process_group()
+    print(f"rank {rank} ok: {done} pivots")
+
+
+if __name__ == "__main__":
+    main()

@@ -198,6 +198,8 @@ def test_optimal_at_start_and_cap():
     ("tall", 1, 1, 3), ("mixed", 1, 5, 3), ("mixed", 3, 60, 10), ("tall", 5, 63, 10),
     ("tall", 257, 64, 30), ("mixed", 300, 191, 30), ("tall", 513, 7, 20),
     ("tall", 1000, 2, 10), ("tall", 2, 5000, 10), ("mixed", 255, 129, 40),
+    # past the persistent kernel's limits: > 256 blocks x 64 rows, > 256 x 256 columns
+    ("tall", 16500, 3, 12), ("tall", 2, 66000, 6),
 ])
 @pytest.mark.parametrize("block", [1, 7, 32])
 def test_ragged_shapes_bit_exact(kind, m, ns, k, block, select_mode):
@@ -230,9 +232,18 @@ def test_cfg3_full_size_bit_exact(block, select_mode):
 
 
 # ------------------------------------------------------------ sharding
-@pytest.mark.parametrize("block", [1, 6])
+@pytest.fixture(params=["peer", "rccl"])
+def shard_mode(request, monkeypatch):
+    """row-sharded pivot selection: one persistent kernel per shard with the
+    device-side exchange (default), or the per-pivot kernels with one
+    (emulated) RCCL collective per pivot"""
+    monkeypatch.setenv("LPGPU_PEER", "1" if request.param == "peer" else "0")
+    return request.param
+
+
+@pytest.mark.parametrize("block", [1, 6, 32])
 @pytest.mark.parametrize("nshards", [1, 2, 3, 5, 8])
-def test_sharded_group_invariance(nshards, block):
+def test_sharded_group_invariance(nshards, block, shard_mode):
     """Row-sharded protocol (allreduce-min + slot allgather) emulated in one
     process: identical sequence and bit-identical rows for any shard count."""
     T = gen.tableau("mixed", 300, 200, 9)
@@ -315,7 +326,7 @@ def test_block_size_invariance(select_mode):
         assert np.array_equal(D, outs[0][1])
 
 
-def test_find_without_pivot_leaves_tableau_untouched():
+def test_find_without_pivot_leaves_tableau_untouched(shard_mode):
     T = gen.tableau("mixed", 64, 64, 8)
     for grp in ([engine_of(T)], _lib.create_group(64, 128, 3)):
         for g in grp:
@@ -344,7 +355,7 @@ def _straddle_tableau():
 @pytest.mark.parametrize("kind,tie,nshards,k", [
     ("straddle", 0.25, 2, 1), ("mixed", 0.25, 3, 40), ("mixed", 0.02, 4, 60), ("tall", 0.1, 5, 40),
 ])
-def test_sharded_one_exchange_band_and_straddle(kind, tie, nshards, k):
+def test_sharded_one_exchange_band_and_straddle(kind, tie, nshards, k, shard_mode):
     """The one-allgather protocol's band test, and its rare two-exchange
     recovery when a near-tie straddles the band (oracle/sharded_model.py)."""
     T = _straddle_tableau() if kind == "straddle" else gen.tableau(kind, 48, 32, 23)
