@@ -129,6 +129,12 @@ def main():
                                                             "hbm_traffic.json"))
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU diagnostic: run the N-rank job's whole tableau on one GPU")
+    ap.add_argument("--exchange", choices=["auto", "peer", "rccl"], default="auto",
+                    help="N > 1: device-side peer exchange per pivot (auto: if its setup "
+                         "check passes on every rank) or one RCCL collective per pivot")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="N > 1 without an RCCL communicator (peer exchange only; lets two "
+                         "ranks share one GPU for testing)")
     ap.add_argument("--group-shards", type=int, default=0,
                     help="1-GPU diagnostic: the N-rank row-sharded job as N in-process shards "
                          "on one GPU (device copies instead of RCCL)")
@@ -154,12 +160,33 @@ def main():
     if world == 1:
         rb, re_ = 0, m
     shards = None
+    exchange = None
     if world > 1:
-        uid = _lib.comm_unique_id() if rank == 0 else None
-        box = [uid]
+        import torch
+        box = [None if args.no_rccl else (_lib.comm_unique_id() if rank == 0 else None)]
         dist.broadcast_object_list(box, src=0)
         eng = _lib.create_sharded(m, n, rank, world, box[0], device=device)
         assert (eng.row_begin, eng.row_count) == (rb, re_ - rb)
+        # device-side exchange between the ranks; every rank must agree on it
+        ok, why = 0, "not requested"
+        if args.exchange != "rccl" or args.no_rccl:
+            try:
+                hs = [None] * world
+                dist.all_gather_object(hs, eng.peer_handle())
+                eng.peer_open(b"".join(hs))
+                ok, why = 1, ""
+            except (_lib.DeviceError, ValueError) as ex:
+                why = str(ex)
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag[0]) == 1:
+            exchange = "device peer stores over xGMI (one persistent selection launch per group)"
+        else:
+            if args.exchange == "peer" or args.no_rccl:
+                raise SystemExit(f"peer exchange unavailable on some rank: {why}")
+            if ok:
+                eng.peer_enable(False)
+            exchange = "RCCL collectives per pivot" + (f" (peer setup failed: {why})" if why else "")
     elif args.group_shards:
         shards = _lib.create_group(m, n, args.group_shards, device=device)
         eng = shards[0]
@@ -227,7 +254,7 @@ def main():
                          + (f" [diagnostic: whole tableau on 1 GPU]" if args.emulate_ranks else "")
                          + (f" [diagnostic: {nsim} in-process shards on 1 GPU]" if args.group_shards else "")),
             "m": m, "n": n, "rows_per_gpu": re_ - rb, "rule": "standard (findPivotStandard)",
-            "parallelism": f"row-shard x{world}" + (" over RCCL" if world > 1 else ""),
+            "parallelism": f"row-shard x{world}" + (f": {exchange}" if world > 1 else ""),
         },
         "lp_pivots_per_s": lp_pps,
         "pivots_per_sweep": args.block,

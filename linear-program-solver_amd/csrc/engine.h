@@ -168,6 +168,7 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
 // row-sharded: every rank writes a tagged granule to every rank's buffer and
 // waits (bounded) for all of them; *ok = 1 if all arrived (peer exchange works)
 hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, int *ok_dev);
+int group_fits(const Args &A, int bmax, int lag_layout, int xr, int nshard);
 #ifndef LPK_GROUP_BLOCKS
 #define LPK_GROUP_BLOCKS 64
 #endif

@@ -766,12 +766,15 @@ static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int g
 
 static int pev_at(lp_handle *h, size_t k, hipEvent_t *e);
 
-// row-sharded persistent selection usable for this shape?
-static bool xr_ok(const lp_handle *h)
+// row-sharded persistent selection usable for this shape?  (In-process
+// shards share one device: all their blocks must fit on it at once.)
+static bool xr_ok(lp_handle *h)
 {
     if (!h->comm || !h->peer_ok || !h->persistent) return false;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
-    return lpk::group_blocks(rcmax, h->ld, h->block, 0) > 0;
+    if (lpk::group_blocks(rcmax, h->ld, h->block, 0) == 0) return false;
+    const Members M = members_of(h);
+    return M.size() == 1 || lpk::group_fits(args_of(h), h->block, 0, 1, (int)M.size()) != 0;
 }
 
 // one persistent selection launch per rank for a group of cnt pivots.  The

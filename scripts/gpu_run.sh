@@ -40,7 +40,8 @@ for step in "$@"; do
                 run bench_cfg4_1gpu_b$B 600 python bench.py --no-cpu-baseline --block $B --emulate-ranks 8 --steps 256
             done ;;
         dist2)
-            run bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 64 --warmup 8 ;;
+            # two ranks sharing the one GPU: no RCCL (it refuses that), peer exchange only
+            run bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 256 --warmup 32 --no-rccl ;;
         prof16)
             export TMPDIR=/tmp
             run rocprof16 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof16" -o run -- python3 "$PWD/bench.py" --steps 512 --block 16 --no-cpu-baseline ;;
