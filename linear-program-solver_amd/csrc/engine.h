@@ -141,8 +141,13 @@ constexpr int NRANK_MAX = 64;
 constexpr long long XS_SUM_PAR = (NRANK_MAX + 1) * 8;            // per parity
 constexpr long long XS_PROW = 2 * XS_SUM_PAR;
 constexpr long long XS_PROW_BLOCK = 2 * 4 * 64;                   // 2 granules x 4 columns x 64 lanes
-constexpr long long XS_LOC = XS_PROW + 256 * XS_PROW_BLOCK;       // GROUP_MAXBLOCKS blocks
-constexpr long long XS_GRANULES = XS_LOC + 256 * 8;
+constexpr long long XS_PROW_RANK = 256 * XS_PROW_BLOCK;           // GROUP_MAXBLOCKS blocks per source rank
+// + 2 parities x nranks x XS_PROW_RANK of pivot-row slices, then the local
+// straddle slots
+__host__ __device__ inline long long xs_granules(int nranks)
+{
+    return XS_PROW + 2LL * nranks * XS_PROW_RANK + 256 * 8;
+}
 
 // launch wrappers (kernels.hip).  t = index of the pivot within its group
 // (known to the host, which enqueues the groups); grp = group parity.

@@ -843,9 +843,11 @@ constexpr int CH = 8;    // deferred pivots applied per chunk (loads issued toge
 // as inside a device).  Layout in granules:
 //   [XS_SUM]   2 parities x (NRANK_MAX + 1) slots x 8: the ranks' leaving-row
 //              summaries (slot NRANK_MAX: a straddle resolution)
-//   [XS_PROW]  GROUP_MAXBLOCKS x 512: the winning rank's pivot row, block b's
-//              columns as {lo, tag}, {hi, tag} granule pairs
-//   [XS_LOC]   GROUP_MAXBLOCKS x 8: this rank's per-block straddle rescans
+//   [XS_PROW]  2 parities x nranks source ranks x GROUP_MAXBLOCKS x 512: each
+//              rank's candidate pivot row, block b's columns as {lo, tag},
+//              {hi, tag} granule pairs (parities: a rank may run one pivot
+//              ahead of a slow reader, never two)
+//   then       GROUP_MAXBLOCKS x 8: this rank's per-block straddle rescans
 template <typename T>
 __device__ __forceinline__ void st_sys(T *p, T v)
 {
@@ -1187,11 +1189,66 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             status = LP_UNBOUNDED;
             break;
         }
+        stamp(A, t, 7);
+        // ---- pivot row on own columns.  prow(Rl, av): the current values of
+        //      local row Rl (stored row + this group's deferred pivots, the
+        //      lagging group's first) divided by the pivot element.  Tableau
+        //      row loads first, then the cross-block loads (one round trip).
+        double pv_[IPL];                  // this pivot's normalised row on own columns
+        const double f0 = ld_sc1(&A.M[mi(A.rows, 0, t)]);
+        auto prow = [&](long long Rl, double avv) {
+            double xv[IPL];
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                const long long j = jc0 + tid + k * nth;
+                xv[k] = j < jc1 ? A.T[Rl * A.ld + j] : 0.0;
+            }
+            if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, Rl, tid)]);
+            if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, Rl, tid)];
+            // pivots s whose pivot row is Rl: the select instead of the FMA (uniform)
+            const u64 rpiv = __ballot(tid < t && sR[tid] == Rl);
+            const u64 rpivp = __ballot(tid < np && sRp[tid] == Rl);
+            __syncthreads();
+            stamp(A, t, 8);
+            const double av = XR ? avv : sMr[t];
+            auto chain_row = [&](int nt, const double *smr, const double *const (&pc)[IPL], u64 piv) {
+                for (int s0 = 0; s0 < nt; s0 += CH) {
+                    double mr[CH], pv[CH][IPL];
+#pragma unroll
+                    for (int u = 0; u < CH; ++u) {
+                        mr[u] = smr[s0 + u];
+#pragma unroll
+                        for (int k = 0; k < IPL; ++k) pv[u][k] = pc[k][s0 + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < CH; ++u)
+                        if (s0 + u < nt) {
+                            if ((piv >> (s0 + u)) & 1) {     // row Rl was pivot row s
+#pragma unroll
+                                for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
+                            } else {
+#pragma unroll
+                                for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
+                            }
+                        }
+                }
+            };
+            chain_row(np, sMrp, pcolp, rpivp);
+            chain_row(t, sMr, pcol, rpiv);
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                const long long j = jc0 + tid + k * nth;
+                pv_[k] = (j == C) ? 1.0 : xv[k] / av;
+            }
+            __syncthreads();      // sMr is reused
+        };
         bool win = true;              // this rank holds the leaving row
         long long rglob = R - 1 + A.rb;
         if constexpr (XR) {
-            // ---- leaving row across ranks: every rank sends (local minimum,
+            // ---- leaving row across ranks.  Every rank sends (local minimum,
             //      candidate's ratio, global row, pivot element) to all ranks
+            //      and, without waiting for the verdict, its candidate's
+            //      normalised row: the winner's row is then already on its way.
             const int par = t & 1;
             const int N = A.nranks;
             u64 *xs = A.xbuf + par * XS_SUM_PAR;           // local slots, written by the peers
@@ -1208,6 +1265,27 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 for (int p = 0; p < N; ++p)
                     st_sys(&A.peer[p][par * XS_SUM_PAR + A.rank * 8 + tid], tg | wv);
             }
+            // this rank's slot of pivot-row slices in every peer's buffer
+            auto send_row = [&](int ph) {
+                const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
+                for (int p = 0; p < N; ++p) {
+                    if (p == A.rank) continue;
+                    u64 *dst = A.peer[p] + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
+                               (long long)b * XS_PROW_BLOCK;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        const int kk = tid + k * nth;
+                        if (jc0 + kk < jc1) {
+                            st_sys(&dst[2 * kk], tg | lo32(pv_[k]));
+                            st_sys(&dst[2 * kk + 1], tg | hi32(pv_[k]));
+                        }
+                    }
+                }
+            };
+            if (R != NONE) {
+                prow(R, aR);
+                send_row(3);
+            }
             unsigned x[7];
             if (!gather_x<7>(xs, N, gtag(seq, t, 2), x, &ctl->bar_timeout)) {
                 status = LP_DEVICE_ERROR;
@@ -1221,6 +1299,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             const double qs = rl_d(x[2], x[3], ps);
             long long rg;
             double as;
+            int ph = 3;                   // the tag of the winner's row slices
             if (qs <= thr) {
                 rg = (long long)rl32(x[4], ps);
                 as = rl_d(x[5], x[6], ps);
@@ -1228,13 +1307,14 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 // rare: a near-tie straddles the band across ranks.  Rank ps
                 // (the first with a row inside it) finds its first such row:
                 // each block offers its first own row, block 0 sends the lowest
-                // to every rank (the straddle slot)
+                // to every rank (the straddle slot); rank ps then ships that
+                // row's normalised values instead of its candidate's
                 if (A.rank == ps) {
                     const u64 mk = __ballot(own && okown && qown <= thr);
                     const int fr = mk ? __builtin_ctzll(mk) : 0;
                     const long long ir = mk ? lr0 + fr : NONE;
                     const double ar = rl_d(lo32(a), hi32(a), fr);
-                    u64 *loc = A.xbuf + XS_LOC;
+                    u64 *loc = A.xbuf + XS_PROW + 2LL * N * XS_PROW_RANK;
                     if (tid < 3) {
                         const unsigned wv = tid == 0 ? idx32(ir) : tid == 1 ? lo32(ar) : hi32(ar);
                         st_sc1(&loc[b * 8 + tid], ((u64)gtag(seq, t, 4) << 32) | wv);
@@ -1272,107 +1352,47 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 }
                 rg = (long long)__builtin_amdgcn_readfirstlane(y[0]);
                 as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
+                ph = 6;
+                if (A.rank == ps) {
+                    prow(rg - A.rb + 1, as);
+                    send_row(6);
+                }
             }
             win = A.rank == ps;
             rglob = rg;
             R = win ? rg - A.rb + 1 : -1;
             aR = as;
-        }
-        if (li == R) ownpiv |= 1ull << t;
-        stamp(A, t, 7);
-        // ---- pivot row on own columns, row 0 on own columns.  Tableau row
-        //      loads first, then the cross-block loads (one round trip).
-        double pv_[IPL];                  // this pivot's normalised row on own columns
-        const double f0 = ld_sc1(&A.M[mi(A.rows, 0, t)]);
-        if (win) {
-            double xv[IPL];
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) {
-                const long long j = jc0 + tid + k * nth;
-                xv[k] = j < jc1 ? A.T[R * A.ld + j] : 0.0;
-            }
-            if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, R, tid)]);
-            if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, R, tid)];
-            if (tid == 0) sR[t] = R;
-            // pivots s whose pivot row is R: the select instead of the FMA (uniform)
-            const u64 rpiv = __ballot(tid < t && sR[tid] == R);
-            const u64 rpivp = __ballot(tid < np && sRp[tid] == R);
-            __syncthreads();
-            stamp(A, t, 8);
-            const double av = XR ? aR : sMr[t];
-            // deferred pivots of the previous group (lag), then 0..t-1 of this
-            // group, on the own columns, CH at a time
-            auto chain_row = [&](int nt, const double *smr, const double *const (&pc)[IPL], u64 piv) {
-                for (int s0 = 0; s0 < nt; s0 += CH) {
-                    double mr[CH], pv[CH][IPL];
-#pragma unroll
-                    for (int u = 0; u < CH; ++u) {
-                        mr[u] = smr[s0 + u];
-#pragma unroll
-                        for (int k = 0; k < IPL; ++k) pv[u][k] = pc[k][s0 + u];
-                    }
-#pragma unroll
-                    for (int u = 0; u < CH; ++u)
-                        if (s0 + u < nt) {
-                            if ((piv >> (s0 + u)) & 1) {     // row R was pivot row s
-#pragma unroll
-                                for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
-                            } else {
-#pragma unroll
-                                for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
-                            }
-                        }
-                }
-            };
-            chain_row(np, sMrp, pcolp, rpivp);
-            chain_row(t, sMr, pcol, rpiv);
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) {
-                const long long j = jc0 + tid + k * nth;
-                pv_[k] = (j == C) ? 1.0 : xv[k] / av;
-            }
-            if constexpr (XR) {
-                // the other ranks' block b gets this block's columns
-                const unsigned long long tg = (u64)gtag(seq, t, 3) << 32;
-                for (int p = 0; p < A.nranks; ++p) {
-                    if (p == A.rank) continue;
-                    u64 *dst = A.peer[p] + XS_PROW + (long long)b * XS_PROW_BLOCK;
+            if (!win) {
+                // the winning rank's block b sent these columns
+                const u64 *src = A.xbuf + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
+                                 (long long)b * XS_PROW_BLOCK;
+                const unsigned tg = gtag(seq, t, ph);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    bool ok = true;
 #pragma unroll
                     for (int k = 0; k < IPL; ++k) {
-                        const int kk = tid + k * nth;
-                        if (jc0 + kk < jc1) {
-                            st_sys(&dst[2 * kk], tg | lo32(pv_[k]));
-                            st_sys(&dst[2 * kk + 1], tg | hi32(pv_[k]));
-                        }
+                        const int kk = min((long long)tid + k * nth, cpb - 1);
+                        const u64 lo = ld_sys(&src[2 * kk]), hi = ld_sys(&src[2 * kk + 1]);
+                        pv_[k] = mk_d((unsigned)lo, (unsigned)hi);
+                        ok = ok && (jc0 + kk >= jc1 ||
+                                    ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
                     }
+                    if (__all(ok)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+                        st_sc1(&ctl->bar_timeout, 1u);
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
+                if (status != LP_PIVOTED) break;
             }
-        } else if constexpr (XR) {
-            if (tid == 0) sR[t] = -1;
-            // the winning rank's block b sends these columns
-            const u64 *src = A.xbuf + XS_PROW + (long long)b * XS_PROW_BLOCK;
-            const unsigned tg = gtag(seq, t, 3);
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-                bool ok = true;
-#pragma unroll
-                for (int k = 0; k < IPL; ++k) {
-                    const int kk = min((long long)tid + k * nth, cpb - 1);
-                    const u64 lo = ld_sys(&src[2 * kk]), hi = ld_sys(&src[2 * kk + 1]);
-                    pv_[k] = mk_d((unsigned)lo, (unsigned)hi);
-                    ok = ok && (jc0 + kk >= jc1 || ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
-                }
-                if (__all(ok)) break;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
-                    st_sc1(&ctl->bar_timeout, 1u);
-                    status = LP_DEVICE_ERROR;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (status != LP_PIVOTED) break;
-            __syncthreads();
+        } else {
+            prow(R, 0.0);
         }
+        if (li == R) ownpiv |= 1ull << t;
+        if (tid == 0) sR[t] = R;
         double vmin = INFINITY, v0 = 0.0;
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {

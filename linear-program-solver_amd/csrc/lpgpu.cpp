@@ -439,7 +439,7 @@ extern "C" int lp_create_group(int64_t m, int64_t n, int device, int nshards, lp
         std::vector<unsigned long long *> xb;
         for (lp_handle *h : grp->all) {
             if (!h->peer_enable || nshards > lpk::NRANK_MAX) break;
-            const size_t xbytes = lpk::XS_GRANULES * sizeof(unsigned long long);
+            const size_t xbytes = lpk::xs_granules(h->nranks) * sizeof(unsigned long long);
             if (hipMalloc(&h->xbuf, xbytes) != hipSuccess || hipMemset(h->xbuf, 0, xbytes) != hipSuccess ||
                 hipStreamCreateWithFlags(&h->sx, hipStreamNonBlocking) != hipSuccess) {
                 g_create_err = "group exchange buffers";
@@ -489,7 +489,7 @@ extern "C" int lp_peer_handle(lp_handle *h, void *ipc64)
 {
     if (!h || !h->comm || h->nranks > lpk::NRANK_MAX) return h ? fail(h, LP_BAD_ARG, "not a sharded handle") : LP_BAD_ARG;
     HCHK(h, hipSetDevice(h->dev));
-    const size_t xbytes = lpk::XS_GRANULES * sizeof(unsigned long long);
+    const size_t xbytes = lpk::xs_granules(h->nranks) * sizeof(unsigned long long);
     hipIpcMemHandle_t hd;
     if (!h->xbuf) {
         // fine-grained: peers' system-scope stores are visible to this device's
@@ -540,7 +540,7 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     (void)hipFree(dok);
     if (e != hipSuccess || e2 != hipSuccess) return fail(h, LP_DEVICE_ERROR, "peer ping launch failed");
     // the ping used the summary slots: clear them for the pivots
-    HCHK(h, hipMemset(h->xbuf, 0, lpk::XS_GRANULES * sizeof(unsigned long long)));
+    HCHK(h, hipMemset(h->xbuf, 0, lpk::xs_granules(h->nranks) * sizeof(unsigned long long)));
     HCHK(h, hipDeviceSynchronize());
     if (!ok) return fail(h, LP_DEVICE_ERROR, "peer exchange check timed out");
     h->peer_ok = true;
