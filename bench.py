@@ -5,12 +5,16 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 One "step" = one simplex pivot (entering scan, ratio test, rank-1 update of
-the whole float64 tableau) with the standard rule, all on the device.
+the whole float64 tableau) with the standard rule, all on the device (the
+rank-1 updates of 32 pivots are applied in one sweep; bit-identical).
 Workload (weak scaling): every GPU holds 4096 constraint rows
 of an 8192-variable tableau.
   N = 1 : cfg3, G_mixed(m=4096, ns=4096, seed 3) -> a 4097 x 8193 tableau
   N > 1 : G_tall(m=4096*N, n=8192, seed 3), rows sharded 4096 per rank
-          (N = 8 is cfg4, the 32768 x 8192 tableau); RCCL exchange per pivot.
+          (N = 8 is cfg4, the 32768 x 8192 tableau).  Per pivot the ranks
+          exchange candidates and the pivot row device-side (peer stores over
+          xGMI inside one persistent selection kernel per group); RCCL
+          collectives per pivot if that exchange cannot be set up.
 ``value`` = pivots/s x N (each pivot sweeps N shards of 4096 x 8192), i.e.
 plain LP pivots/s at N = 1; ``lp_pivots_per_s`` is the LP-level rate.
 
@@ -206,7 +210,33 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    st, done = eng.run(_lib.RULE_STANDARD, args.warmup)     # ends with a stream sync
+    def upload():
+        for e in (shards or [eng]):
+            e.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
+            a0, a1 = (e.row_begin, e.row_begin + e.row_count) if shards else (rb, re_)
+            for a in range(a0, a1, blk):
+                e.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + min(a + blk, a1)))
+
+    try:
+        st, done = eng.run(_lib.RULE_STANDARD, args.warmup)     # ends with a stream sync
+        warm_ok = 1
+    except _lib.DeviceError as ex:
+        if dist is None or exchange is None or not exchange.startswith("device"):
+            raise
+        warm_ok, why = 0, str(ex)
+    if dist is not None and exchange is not None and exchange.startswith("device"):
+        import torch
+        flag = torch.tensor([warm_ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag[0]) == 0:
+            # the peer exchange failed on some rank: every rank starts over on
+            # the RCCL per-pivot path (identical results)
+            if args.no_rccl:
+                raise SystemExit("peer exchange failed during warmup and there is no RCCL communicator")
+            eng.peer_enable(False)
+            exchange = "RCCL collectives per pivot (peer exchange failed in warmup)"
+            upload()
+            st, done = eng.run(_lib.RULE_STANDARD, args.warmup)
     if done != args.warmup:
         raise SystemExit(f"warmup ended early: status {st} after {done} pivots")
     barrier()
