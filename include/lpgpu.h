@@ -144,6 +144,25 @@ int lp_solve(lp_handle *h, int64_t max_pivots, int64_t *npiv, int64_t *nstd);
  * unbounded.  Returns the last status; *done = pivots performed. */
 int lp_run(lp_handle *h, int rule, int64_t k, int64_t *done);
 
+/* findPivotMaxIncrease (simplex.py:286-328): over columns with c_j < -cost,
+ * the largest objective increase -c_j * (min ratio of column j); ties to the
+ * first column, its ratio-test row.  LP_UNBOUNDED if any such column has no
+ * eligible row (the reference returns at the first one, :319-320),
+ * LP_OPTIMAL if no column qualifies; performs the pivot if do_pivot.  Not on
+ * multi-process sharded handles (LP_BAD_ARG). */
+int lp_find_pivot_max_increase(lp_handle *h, int do_pivot, int64_t *r, int64_t *c);
+
+/* findPivotAll (simplex.py:330-360): every min-ratio pivot of every column,
+ * column-major, rows in order; writes up to cap (r, c) pairs, *count = all. */
+int lp_find_pivot_all(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count);
+
+/* Form checks of the current tableau, exact comparisons of the float64 values
+ * (tableau.py:466-521): flags[0] isCanonical, [1] isOptimal, [2] isUnbounded,
+ * [3] isInfeasible, [4] isDegenerate.  bcols (m entries, may be NULL) gets
+ * isCanonical's basic column per row (-1: none) unless some b_i < 0, where
+ * the reference leaves it untouched. */
+int lp_form_checks(lp_handle *h, int32_t *flags, int64_t *bcols);
+
 /* Pivot log of the last lp_solve / lp_run: (r, c) pairs, oldest first.  The
  * front-end replays it to maintain Simplex._bfs and the variable marks
  * (simplex.py:192-197).  *count = pivots available (may exceed cap). */

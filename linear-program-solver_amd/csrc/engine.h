@@ -214,6 +214,22 @@ __host__ __device__ inline long long group_blocks(long long rc, long long ld, in
     return group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX ? 0 : g;
 }
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
+
+// per-column statistics of the local constraint rows (row 0 excluded)
+struct ColStat {
+    double gmin;         // minimum ratio over rows with a > tol.pivot (INFINITY: none)
+    long long npos;      // rows with a > tol.pivot
+    long long npos0;     // rows with a > 0
+    long long nnz;       // rows with a != 0
+    long long none;      // rows with a == 1
+    long long one_row;   // first such row (global constraint index) or NONE
+    long long nneg;      // rows with a < 0
+    long long pad;
+};
+hipError_t launch_colstat(hipStream_t s, const Args &A, ColStat *out);   // out[ld]
+hipError_t launch_colband(hipStream_t s, const Args &A, const double *thr, long long *first,
+                          long long *count, const long long *offs, long long *pairs);
+hipError_t launch_rowpos(hipStream_t s, const Args &A, int *rowpos);     // rowpos[rc]
 hipError_t launch_resume(hipStream_t s, const Args &A);
 __host__ __device__ inline int ratio_blocks(long long rows)
 {

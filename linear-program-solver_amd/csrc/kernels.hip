@@ -1620,6 +1620,123 @@ __global__ void k_peer_ping(Args A, unsigned tag, int *ok)
     if (threadIdx.x == 0) *ok = all ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Column scans (findPivotMaxIncrease / findPivotAll, simplex.py:286-360) and
+// form checks (tableau.py:466-521): per column of the local constraint rows,
+// one pass over the (current) tableau.  Block = 64 columns x 4 waves of rows,
+// rows read coalesced across the lanes.
+// ---------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(256) k_colstat(Args A, ColStat *out)
+{
+    __shared__ ColStat part[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long long j = (long long)blockIdx.x * 64 + lane;
+    ColStat c;
+    c.gmin = INFINITY;
+    c.npos = c.npos0 = c.nnz = c.none = c.nneg = 0;
+    c.one_row = NONE;
+    c.pad = 0;
+    if (j < A.ld)
+        for (long long li = 1 + wave; li < A.rows; li += 4) {
+            const double x = A.T[li * A.ld + j];
+            bool ok;
+            const double q = row_ratio(x, A.T[li * A.ld], A.tol, ok);
+            if (ok) {
+                c.npos += 1;
+                c.gmin = fmin(c.gmin, q);
+            }
+            c.npos0 += x > 0.0;
+            c.nnz += x != 0.0;
+            c.nneg += x < 0.0;
+            if (x == 1.0) {
+                c.none += 1;
+                if (c.one_row == NONE) c.one_row = li - 1 + A.rb;
+            }
+        }
+    part[wave][lane] = c;
+    __syncthreads();
+    if (wave == 0 && j < A.ld) {
+        for (int w = 1; w < 4; ++w) {
+            const ColStat &d = part[w][lane];
+            c.gmin = fmin(c.gmin, d.gmin);
+            c.npos += d.npos;
+            c.npos0 += d.npos0;
+            c.nnz += d.nnz;
+            c.nneg += d.nneg;
+            c.none += d.none;
+            c.one_row = d.one_row < c.one_row ? d.one_row : c.one_row;
+        }
+        out[j] = c;
+    }
+}
+
+// rows inside each column's ratio band (thr[j] = INFINITY: none), in row
+// order: first[j] = the first (global index), count[j]; with pairs != nullptr
+// the (row, variable) pairs of column j go to pairs[2 * (offs[j] + k)]
+__global__ void __launch_bounds__(64) k_colband(Args A, const double *thr, long long *first,
+                                               long long *count, const long long *offs,
+                                               long long *pairs)
+{
+    const long long j = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (j >= A.ld) return;
+    const double th = thr[j];
+    long long f = NONE, k = 0;
+    if (th < INFINITY)
+        for (long long li = 1; li < A.rows; ++li) {
+            bool ok;
+            const double q = row_ratio(A.T[li * A.ld + j], A.T[li * A.ld], A.tol, ok);
+            if (ok && q <= th) {
+                const long long rg = li - 1 + A.rb;
+                if (f == NONE) f = rg;
+                if (pairs) {
+                    pairs[2 * (offs[j] + k)] = rg;
+                    pairs[2 * (offs[j] + k) + 1] = j - 1;
+                }
+                ++k;
+            }
+        }
+    first[j] = f;
+    count[j] = k;
+}
+
+// per local constraint row: b_i > 0 and every a_ij <= 0 (isInfeasible,
+// tableau.py:510-514)
+__global__ void __launch_bounds__(256) k_rowpos(Args A, int *rowpos)
+{
+    __shared__ int any;
+    const long long li = 1 + blockIdx.x;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    int mine = 0;
+    for (long long j = 1 + threadIdx.x; j <= A.n; j += blockDim.x)
+        mine |= A.T[li * A.ld + j] > 0.0;
+    if (mine) any = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) rowpos[li - 1] = (A.T[li * A.ld] > 0.0 && !any) ? 1 : 0;
+}
+
+hipError_t launch_colstat(hipStream_t s, const Args &A, ColStat *out)
+{
+    hipLaunchKernelGGL(k_colstat, dim3((unsigned)((A.ld + 63) / 64)), dim3(256), 0, s, A, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_colband(hipStream_t s, const Args &A, const double *thr, long long *first,
+                          long long *count, const long long *offs, long long *pairs)
+{
+    hipLaunchKernelGGL(k_colband, dim3((unsigned)((A.ld + 63) / 64)), dim3(64), 0, s, A, thr, first,
+                       count, offs, pairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_rowpos(hipStream_t s, const Args &A, int *rowpos)
+{
+    if (A.rc < 1) return hipSuccess;
+    hipLaunchKernelGGL(k_rowpos, dim3((unsigned)A.rc), dim3(256), 0, s, A, rowpos);
+    return hipGetLastError();
+}
+
 __global__ void k_resume(Ctl *ctl)
 {
     ctl->status = LP_PIVOTED;

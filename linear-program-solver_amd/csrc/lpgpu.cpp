@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -61,6 +62,11 @@ struct lp_handle {
     bool peer_ok = false;                   // the exchange is set up and validated
     bool peer_enable = true;                // LPGPU_PEER=0 keeps the RCCL per-pivot path
     hipStream_t sx = nullptr;               // in-process shards: own stream for the persistent launch
+    // column scans / form checks (allocated on first use)
+    lpk::ColStat *cstat = nullptr;
+    double *cthr = nullptr;
+    long long *cfirst = nullptr, *ccount = nullptr, *coffs = nullptr;
+    int *rowflag = nullptr;
     bool eager_ok = false;          // row0/col0 mirror the stored tableau
     Ctl *ctl = nullptr;
     Ctl *hctl = nullptr;            // pinned mirror
@@ -571,6 +577,9 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->s) (void)hipStreamSynchronize(h->s);
     for (hipEvent_t e : h->ev) (void)hipEventDestroy(e);
     if (h->sx) (void)hipStreamSynchronize(h->sx);
+    for (void *p : {(void *)h->cstat, (void *)h->cthr, (void *)h->cfirst, (void *)h->ccount,
+                    (void *)h->coffs, (void *)h->rowflag})
+        if (p) (void)hipFree(p);
     for (void *p : h->ipc_open) (void)hipIpcCloseMemHandle(p);
     if (h->dpeer) (void)hipFree(h->dpeer);
     if (h->xbuf) (void)hipFree(h->xbuf);
@@ -1136,6 +1145,215 @@ extern "C" int lp_pivot(lp_handle *h, int64_t r, int64_t c) { return explicit_pi
 extern "C" int lp_pivot_checked(lp_handle *h, int64_t r, int64_t c)
 {
     return explicit_pivot(h, r, c, true);
+}
+
+// ---------------------------------------------------------------------------
+// column scans: findPivotMaxIncrease, findPivotAll, form checks.  The stored
+// tableau is current at every API boundary (each call sweeps its pending
+// pivots).  Shards of one process are combined on the host in rank order; a
+// multi-process sharded handle would need a collective here (not provided).
+// ---------------------------------------------------------------------------
+
+static int scan_members(lp_handle *h, Members &M)
+{
+    M = members_of(h);
+    if (h->comm && M.size() == 1 && h->nranks > 1)
+        return fail(h, LP_BAD_ARG, "column scans are not available on a multi-process sharded handle");
+    for (lp_handle *x : M) {
+        HCHK(x, hipSetDevice(x->dev));
+        if (!x->eager_ok) {                  // row 0 / column 0 mirrors after an upload
+            HCHK(x, lpk::launch_load_eager(x->s, args_of(x)));
+            x->eager_ok = true;
+        }
+        if (!x->cstat) {
+            HCHK(x, hipMalloc(&x->cstat, x->ld * sizeof(lpk::ColStat)));
+            HCHK(x, hipMalloc(&x->cthr, x->ld * sizeof(double)));
+            HCHK(x, hipMalloc(&x->cfirst, x->ld * sizeof(long long)));
+            HCHK(x, hipMalloc(&x->ccount, x->ld * sizeof(long long)));
+            HCHK(x, hipMalloc(&x->coffs, x->ld * sizeof(long long)));
+            HCHK(x, hipMalloc(&x->rowflag, std::max<int64_t>(x->rc, 1) * sizeof(int)));
+        }
+    }
+    return LP_PIVOTED;
+}
+
+// per-column statistics over every shard, and the current row 0
+static int column_stats(lp_handle *h, const Members &M, std::vector<lpk::ColStat> &cs,
+                        std::vector<double> &row0)
+{
+    row0.assign(h->ld, 0.0);
+    HCHK(h, hipMemcpyAsync(row0.data(), M[0]->row0, h->ld * sizeof(double), hipMemcpyDeviceToHost,
+                           M[0]->s));
+    std::vector<lpk::ColStat> part(h->ld);
+    for (size_t k = 0; k < M.size(); ++k) {
+        lp_handle *x = M[k];
+        HCHK(x, lpk::launch_colstat(x->s, args_of(x), x->cstat));
+        HCHK(x, hipMemcpyAsync(part.data(), x->cstat, x->ld * sizeof(lpk::ColStat),
+                               hipMemcpyDeviceToHost, x->s));
+        HCHK(x, hipStreamSynchronize(x->s));
+        if (k == 0) {
+            cs = part;
+            continue;
+        }
+        for (int64_t j = 0; j < h->ld; ++j) {
+            lpk::ColStat &c = cs[j];
+            const lpk::ColStat &d = part[j];
+            c.gmin = std::min(c.gmin, d.gmin);
+            c.npos += d.npos;
+            c.npos0 += d.npos0;
+            c.nnz += d.nnz;
+            c.nneg += d.nneg;
+            c.none += d.none;
+            c.one_row = std::min(c.one_row, d.one_row);
+        }
+    }
+    return LP_PIVOTED;
+}
+
+// rows inside the band thr[j] of every shard: first[j] (global, first shard
+// in rank order that has one) and per-shard counts
+static int band_pass(lp_handle *h, const Members &M, const std::vector<double> &thr,
+                     std::vector<long long> &first, std::vector<std::vector<long long>> &counts)
+{
+    first.assign(h->ld, lpk::NONE);
+    counts.assign(M.size(), std::vector<long long>(h->ld, 0));
+    std::vector<long long> f(h->ld);
+    for (size_t k = 0; k < M.size(); ++k) {
+        lp_handle *x = M[k];
+        HCHK(x, hipMemcpyAsync(x->cthr, thr.data(), x->ld * sizeof(double), hipMemcpyHostToDevice, x->s));
+        HCHK(x, lpk::launch_colband(x->s, args_of(x), x->cthr, x->cfirst, x->ccount, nullptr, nullptr));
+        HCHK(x, hipMemcpyAsync(f.data(), x->cfirst, x->ld * sizeof(long long), hipMemcpyDeviceToHost, x->s));
+        HCHK(x, hipMemcpyAsync(counts[k].data(), x->ccount, x->ld * sizeof(long long),
+                               hipMemcpyDeviceToHost, x->s));
+        HCHK(x, hipStreamSynchronize(x->s));
+        for (int64_t j = 0; j < h->ld; ++j)
+            if (first[j] == lpk::NONE) first[j] = f[j];
+    }
+    return LP_PIVOTED;
+}
+
+static double band_of(double g, double tie) { return g + tie * std::fabs(g); }
+
+extern "C" int lp_find_pivot_max_increase(lp_handle *h, int do_pivot, int64_t *r, int64_t *c)
+{
+    *r = -1;
+    *c = -1;
+    Members M;
+    CALL(scan_members(h, M));
+    std::vector<lpk::ColStat> cs;
+    std::vector<double> row0;
+    CALL(column_stats(h, M, cs, row0));
+    const lp_tol &tol = h->tol;
+    bool any_neg = false;
+    double best = -INFINITY;
+    std::vector<double> inc(h->n + 1, -INFINITY);
+    for (int64_t j = 1; j <= h->n; ++j) {
+        if (!(row0[j] < -tol.cost)) continue;
+        any_neg = true;
+        if (cs[j].npos == 0) return LP_UNBOUNDED;        // simplex.py:319-320
+        inc[j] = -row0[j] * cs[j].gmin;
+        best = std::max(best, inc[j]);
+    }
+    if (!any_neg) return LP_OPTIMAL;
+    const double lim = best - tol.ratio_tie * std::fabs(best);
+    int64_t js = 1;
+    while (!(inc[js] >= lim)) ++js;
+    std::vector<double> thr(h->ld, INFINITY);
+    thr[js] = band_of(cs[js].gmin, tol.ratio_tie);
+    std::vector<long long> first;
+    std::vector<std::vector<long long>> counts;
+    CALL(band_pass(h, M, thr, first, counts));
+    *r = first[js];
+    *c = js - 1;
+    if (do_pivot) {
+        const int st = lp_pivot(h, *r, *c);
+        if (st != LP_PIVOTED) return st;
+    }
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_find_pivot_all(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count)
+{
+    *count = 0;
+    Members M;
+    CALL(scan_members(h, M));
+    std::vector<lpk::ColStat> cs;
+    std::vector<double> row0;
+    CALL(column_stats(h, M, cs, row0));
+    std::vector<double> thr(h->ld, INFINITY);
+    for (int64_t j = 1; j <= h->n; ++j)
+        if (cs[j].npos > 0) thr[j] = band_of(cs[j].gmin, h->tol.ratio_tie);
+    std::vector<long long> first;
+    std::vector<std::vector<long long>> counts;
+    CALL(band_pass(h, M, thr, first, counts));
+    // column-major, shards (= rows) in order within a column
+    std::vector<std::vector<long long>> offs(M.size(), std::vector<long long>(h->ld, 0));
+    long long total = 0;
+    for (int64_t j = 1; j <= h->n; ++j)
+        for (size_t k = 0; k < M.size(); ++k) {
+            offs[k][j] = total;
+            total += counts[k][j];
+        }
+    *count = total;
+    if (total == 0 || cap <= 0) return LP_PIVOTED;
+    long long *pairs = nullptr;
+    HCHK(h, hipMalloc(&pairs, (size_t)total * 2 * sizeof(long long)));
+    for (size_t k = 0; k < M.size(); ++k) {
+        lp_handle *x = M[k];
+        HCHK(x, hipMemcpyAsync(x->cthr, thr.data(), x->ld * sizeof(double), hipMemcpyHostToDevice, x->s));
+        HCHK(x, hipMemcpyAsync(x->coffs, offs[k].data(), x->ld * sizeof(long long),
+                               hipMemcpyHostToDevice, x->s));
+        HCHK(x, lpk::launch_colband(x->s, args_of(x), x->cthr, x->cfirst, x->ccount, x->coffs, pairs));
+        HCHK(x, hipStreamSynchronize(x->s));
+    }
+    const long long keep = std::min<long long>(total, cap);
+    const hipError_t e = hipMemcpy(rc, pairs, (size_t)keep * 2 * sizeof(long long), hipMemcpyDeviceToHost);
+    (void)hipFree(pairs);
+    HCHK(h, e);
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_form_checks(lp_handle *h, int32_t *flags, int64_t *bcols)
+{
+    Members M;
+    CALL(scan_members(h, M));
+    std::vector<lpk::ColStat> cs;
+    std::vector<double> row0;
+    CALL(column_stats(h, M, cs, row0));
+    int infeasible = 0;
+    std::vector<int> rf;
+    for (lp_handle *x : M) {
+        rf.assign(std::max<int64_t>(x->rc, 1), 0);
+        HCHK(x, lpk::launch_rowpos(x->s, args_of(x), x->rowflag));
+        HCHK(x, hipMemcpyAsync(rf.data(), x->rowflag, x->rc * sizeof(int), hipMemcpyDeviceToHost, x->s));
+        HCHK(x, hipStreamSynchronize(x->s));
+        for (int64_t i = 0; i < x->rc; ++i) infeasible |= rf[i];
+    }
+    // isCanonical (tableau.py:466-496): b >= 0, then per row the first column
+    // with zero reduced cost that is a unit vector with its 1 there
+    const bool ok_b = cs[0].nneg == 0;
+    std::vector<int64_t> found(h->m, -1);
+    if (ok_b)
+        for (int64_t j = 1; j <= h->n; ++j)
+            if (row0[j] == 0.0 && cs[j].nnz == 1 && cs[j].none == 1) {
+                const long long i = cs[j].one_row;
+                if (i >= 0 && i < h->m && found[i] == -1) found[i] = j - 1;
+            }
+    bool canonical = ok_b;
+    for (int64_t i = 0; i < h->m && canonical; ++i) canonical = found[i] != -1;
+    if (ok_b && bcols)                       // the reference leaves bcols alone when b < 0
+        for (int64_t i = 0; i < h->m; ++i) bcols[i] = found[i];
+    bool optimal = true, unbounded = false;
+    for (int64_t j = 1; j <= h->n; ++j) {
+        optimal = optimal && row0[j] >= 0.0;                          // tableau.py:500-502
+        unbounded = unbounded || (row0[j] < 0.0 && cs[j].npos0 == 0);  // :504-508
+    }
+    flags[0] = canonical;
+    flags[1] = optimal;
+    flags[2] = unbounded;
+    flags[3] = infeasible;                                  // :510-514
+    flags[4] = cs[0].nnz < h->m;                            // :516-518: some b_i == 0
+    return LP_PIVOTED;
 }
 
 extern "C" int lp_pivot_log(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count)

@@ -72,6 +72,9 @@ _PROTOS = {
     "lp_profile": (C.c_int, [_H, C.c_int]),
     "lp_update_time": (C.c_int, [_H, _PD, _P64]),
     "lp_select_time": (C.c_int, [_H, _PD, _P64]),
+    "lp_find_pivot_max_increase": (C.c_int, [_H, C.c_int, _P64, _P64]),
+    "lp_find_pivot_all": (C.c_int, [_H, _P64, _I64, _P64]),
+    "lp_form_checks": (C.c_int, [_H, C.POINTER(C.c_int32), _P64]),
     "lp_peer_handle": (C.c_int, [_H, C.c_char_p]),
     "lp_peer_open": (C.c_int, [_H, C.c_char_p]),
     "lp_peer_enable": (C.c_int, [_H, C.c_int]),
@@ -233,6 +236,40 @@ class Engine:
         if st != PIVOTED:
             raise DeviceError(f"unexpected status {STATUS_NAMES.get(st, st)}")
         return r.value, c.value
+
+    def find_max_increase(self, do_pivot: bool):
+        """findPivotMaxIncrease -> (r, c) | 'optimal' | 'unbounded'"""
+        r, c = C.c_int64(), C.c_int64()
+        st = self._check(self.lib.lp_find_pivot_max_increase(self.h, int(bool(do_pivot)),
+                                                             C.byref(r), C.byref(c)), self.h)
+        if st == OPTIMAL:
+            return "optimal"
+        if st == UNBOUNDED:
+            return "unbounded"
+        if st != PIVOTED:
+            raise DeviceError(f"unexpected status {STATUS_NAMES.get(st, st)}")
+        return r.value, c.value
+
+    def find_all(self) -> list[tuple[int, int]]:
+        """findPivotAll -> [(r, c), ...] column-major"""
+        cnt = C.c_int64()
+        self._check(self.lib.lp_find_pivot_all(self.h, None, 0, C.byref(cnt)), self.h)
+        if cnt.value == 0:
+            return []
+        out = np.zeros(2 * cnt.value, dtype=np.int64)
+        self._check(self.lib.lp_find_pivot_all(self.h, out.ctypes.data_as(_P64), cnt.value,
+                                               C.byref(cnt)), self.h)
+        return [(int(out[2 * k]), int(out[2 * k + 1])) for k in range(cnt.value)]
+
+    def form_checks(self):
+        """-> dict(canonical, optimal, unbounded, infeasible, degenerate, bcols)"""
+        flags = (C.c_int32 * 5)()
+        bcols = np.full(self.m, -2, dtype=np.int64)
+        self._check(self.lib.lp_form_checks(self.h, flags, bcols.ctypes.data_as(_P64)), self.h)
+        keys = ("canonical", "optimal", "unbounded", "infeasible", "degenerate")
+        out = {k: bool(flags[i]) for i, k in enumerate(keys)}
+        out["bcols"] = None if np.all(bcols == -2) and self.m else [int(x) for x in bcols]
+        return out
 
     def solve(self, max_pivots: int = -1):
         """-> (status, npiv, nstd)"""

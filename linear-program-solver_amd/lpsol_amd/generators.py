@@ -165,3 +165,64 @@ def klee_minty(d: int, degenerate: bool = False) -> np.ndarray:
         T[i, d + i] = 1.0
         T[i, 0] = 0.0 if (degenerate and i % 2 == 0) else float(5 ** i)
     return T
+
+
+# ---------------------------------------------------------------------------
+# LPs that need phase 1 (Simplex._find_bfs, simplex.py:36-108): general
+# constraints with x0 >= 0 a known feasible point, all values dyadic.
+#   eq   : A x = b (no slacks), plus sum x = S (bounds the region)
+#   ge   : A x >= b with surplus columns (-1), plus sum x <= S with a slack
+#   neg  : A x <= b with slacks, some b_i < 0 (phase 1 flips those rows)
+#   dep  : eq plus a repeated row (linearly dependent: the reference raises
+#          IndexError there, simplex.py:93)
+#   infeasible : sum x = 1 and sum x = 2
+# ---------------------------------------------------------------------------
+
+def phase1_lp(kind: str, m: int, ns: int, seed: int, Q: int = 64) -> np.ndarray:
+    if kind == "infeasible":
+        T = np.zeros((3, ns + 1))
+        T[0, 1:] = -1.0
+        T[1:, 1:] = 1.0
+        T[1, 0], T[2, 0] = 1.0, 2.0
+        return T
+    idx = np.arange(m * ns, dtype=np.uint64)
+    A = uint_range(seed, S_A, idx, -Q, Q).reshape(m, ns) / Q
+    x0 = uint_range(seed, 7, np.arange(ns, dtype=np.uint64), 0, 4) / 4.0
+    c = -uint_range(seed, S_C, np.arange(ns, dtype=np.uint64), 1, Q) / Q
+    S = float(np.sum(x0)) + 1.0
+    if kind in ("eq", "dep"):
+        b = A @ x0
+        rows_a = [A, np.ones((1, ns))]
+        rows_b = [b, [float(np.sum(x0))]]
+        if kind == "dep":
+            rows_a.append(A[:1])
+            rows_b.append(b[:1])
+        Af = np.vstack(rows_a)
+        bf = np.concatenate([np.asarray(r, dtype=np.float64) for r in rows_b])
+        cf = c
+    elif kind == "ge":
+        b = A @ x0 - uint_range(seed, S_B, np.arange(m, dtype=np.uint64), 0, 2) / 4.0
+        Af = np.zeros((m + 1, ns + m + 1))
+        Af[:m, :ns] = A
+        Af[:m, ns:ns + m] = -np.eye(m)
+        Af[m, :ns] = 1.0
+        Af[m, ns + m] = 1.0
+        bf = np.concatenate([b, [S]])
+        cf = np.concatenate([c, np.zeros(m + 1)])
+    elif kind == "neg":
+        b = A @ x0 + uint_range(seed, S_B, np.arange(m, dtype=np.uint64), 0, 2) / 4.0
+        Af = np.zeros((m + 1, ns + m + 1))
+        Af[:m, :ns] = A
+        Af[:m, ns:ns + m] = np.eye(m)
+        Af[m, :ns] = 1.0
+        Af[m, ns + m] = 1.0
+        bf = np.concatenate([b, [S]])
+        cf = np.concatenate([c, np.zeros(m + 1)])
+    else:
+        raise ValueError(kind)
+    T = np.zeros((Af.shape[0] + 1, Af.shape[1] + 1))
+    T[0, 1:] = cf
+    T[1:, 0] = bf
+    T[1:, 1:] = Af
+    assert np.all(T * 4096 == np.round(T * 4096))     # dyadic: exact in float64
+    return T

@@ -79,6 +79,10 @@ class Simplex:
         assert all(0 <= j < n for j in self._bfs), \
             'invalid basic feasible solution (internal error)'
         tab._drop([i for i in range(m) if keep[i]], n)
+        # b_i of rows whose artificial left the basis at 0 can carry a rounding
+        # residue of either sign (exactly 0 in the reference): snap to +0 so
+        # the canonical-form check below (b >= 0) holds as it does there
+        tab._snap_b(tol.zero)
         tab.setZ(orig_z)
         tab.setC(orig_c)
         for i, j in enumerate(self._bfs):
@@ -182,15 +186,24 @@ class Simplex:
 
     def findPivotMaxIncrease(self, do_pivot: bool = False):
         '''
-        simplex.py:286-328 -- not on the device yet.
+        the pivot with the largest objective increase among negative reduced
+        costs (simplex.py:286-328): one device scan of every column.
+        'unbounded' as soon as any negative-cost column has no positive
+        entry (:319-320); 'optimal' if there is no negative cost.
         '''
-        raise NotImplementedError('findPivotMaxIncrease is not implemented on the device yet')
+        tab = self._tab
+        res = tab._engine().find_max_increase(do_pivot)
+        if do_pivot and isinstance(res, tuple):
+            tab._device_changed()
+            self._mark(*res)
+        return res
 
-    def findPivotAll(self):
+    def findPivotAll(self) -> list[tuple[int, int]]:
         '''
-        simplex.py:330-360 -- not on the device yet.
+        every min-ratio pivot of every column, column-major, rows in order
+        (simplex.py:330-360): one device scan of every column.
         '''
-        raise NotImplementedError('findPivotAll is not implemented on the device yet')
+        return self._tab._engine().find_all()
 
     # ---------------------------------------------------------- printing
     def __str__(self) -> str:

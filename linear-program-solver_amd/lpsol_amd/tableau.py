@@ -296,6 +296,14 @@ class Tableau:
         self._cm = self._cm[:ncols]
         self._dev_ok = False
 
+    def _snap_b(self, zero: float):
+        """Set b_i with |b_i| <= zero to +0 (phase-1 clean-up)."""
+        T = self._host()
+        small = np.abs(T[1:, 0]) <= zero
+        if small.any():
+            self._touch()
+            self._T[1:, 0][small] = 0.0
+
     # ------------------------------------------------------- row operations
     # Host edits of the mirror used by phase 1 and user code (tableau.py:254-293).
     # The pivot (below) never goes through them: it runs on the device.
@@ -444,7 +452,21 @@ class Tableau:
 
     # ------------------------------------------------------------ form checks
     # Read-only scans of the mirrored tableau (tableau.py:466-521).
+    # form checks (tableau.py:466-521), exact comparisons of the float64
+    # values.  When the device copy is the current one (after pivots) they run
+    # as one device column scan instead of downloading the tableau.
+    def _device_form(self):
+        if self._dev_ok and not self._host_ok and self._eng is not None:
+            return self._eng.form_checks()
+        return None
+
     def isCanonical(self, bcols: list[int] | None = None) -> bool:
+        f = self._device_form()
+        if f is not None:
+            if bcols is not None and f["bcols"] is not None:
+                for i in range(self._m):
+                    bcols[i] = f["bcols"][i]
+            return f["canonical"]
         T = self._host()
         m = self._m
         A = T[1:, 1:]
@@ -466,15 +488,27 @@ class Tableau:
         return all(j != -1 for j in found)
 
     def isOptimal(self) -> bool:
+        f = self._device_form()
+        if f is not None:
+            return f["optimal"]
         return bool(np.all(self._host()[0, 1:] >= 0.0))
 
     def isUnbounded(self) -> bool:
+        f = self._device_form()
+        if f is not None:
+            return f["unbounded"]
         T = self._host()
         return bool(np.any((T[0, 1:] < 0.0) & np.all(T[1:, 1:] <= 0.0, axis=0)))
 
     def isInfeasible(self) -> bool:
+        f = self._device_form()
+        if f is not None:
+            return f["infeasible"]
         T = self._host()
         return bool(np.any((T[1:, 0] > 0.0) & np.all(T[1:, 1:] <= 0.0, axis=1)))
 
     def isDegenerate(self) -> bool:
+        f = self._device_form()
+        if f is not None:
+            return f["degenerate"]
         return bool(np.any(self._host()[1:, 0] == 0.0))

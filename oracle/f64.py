@@ -37,7 +37,10 @@ def lib():
         L.lpf_find.argtypes = [_PD, _I64, _I64, _I64, C.c_int, C.POINTER(Tol), _P64, _P64]
         L.lpf_run.argtypes = [_PD, _I64, _I64, _I64, C.c_int, C.POINTER(Tol), _I64, _P64, _P64]
         L.lpf_solve.argtypes = [_PD, _I64, _I64, _I64, C.POINTER(Tol), _I64, _P64, _P64, _P64]
-        for f in (L.lpf_pivot, L.lpf_find, L.lpf_run, L.lpf_solve):
+        L.lpf_find_max_increase.argtypes = [_PD, _I64, _I64, _I64, C.POINTER(Tol), _P64, _P64]
+        L.lpf_find_all.argtypes = [_PD, _I64, _I64, _I64, C.POINTER(Tol), _P64, _I64]
+        L.lpf_find_all.restype = _I64
+        for f in (L.lpf_pivot, L.lpf_find, L.lpf_run, L.lpf_solve, L.lpf_find_max_increase):
             f.restype = C.c_int
         _lib = L
     return _lib
@@ -73,6 +76,23 @@ class F64Tableau:
         if st == UNBOUNDED:
             return "unbounded"
         return r.value, c.value
+
+    def find_max_increase(self):
+        r, c = C.c_int64(), C.c_int64()
+        st = lib().lpf_find_max_increase(self._p(), self.m, self.n, self.n + 1, C.byref(self.tol),
+                                         C.byref(r), C.byref(c))
+        if st == OPTIMAL:
+            return "optimal"
+        if st == UNBOUNDED:
+            return "unbounded"
+        return r.value, c.value
+
+    def find_all(self):
+        cnt = lib().lpf_find_all(self._p(), self.m, self.n, self.n + 1, C.byref(self.tol), None, 0)
+        out = np.zeros(2 * max(cnt, 1), dtype=np.int64)
+        lib().lpf_find_all(self._p(), self.m, self.n, self.n + 1, C.byref(self.tol),
+                           out.ctypes.data_as(_P64), cnt)
+        return [(int(out[2 * k]), int(out[2 * k + 1])) for k in range(cnt)]
 
     def run(self, rule, k):
         log = np.zeros(2 * max(k, 1), dtype=np.int64)

@@ -34,6 +34,9 @@ def fixture_input(fx):
         e = fx["exact"]
         rows = exact.from_strings(e["z"], e["c"], e["b"], e["a"])
         return np.array([[float(x) for x in r] for r in rows])
+    if "phase1" in fx:
+        g = fx["phase1"]
+        return gen.phase1_lp(g["kind"], g["m"], g["ns"], g["seed"])
     return np.asarray(fx["array"], dtype=np.float64)
 
 

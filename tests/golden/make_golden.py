@@ -107,6 +107,10 @@ def source_of(spec):
         rows = exact.from_strings(e["z"], e["c"], e["b"], e["a"])
         T = np.array([[float(x) for x in r] for r in rows])
         return T, rows
+    if "phase1" in spec:
+        g = spec["phase1"]
+        T = gen.phase1_lp(g["kind"], g["m"], g["ns"], g["seed"])
+        return T, exact.from_array(T)
     T = np.asarray(spec["array"], dtype=np.float64)
     return T, exact.from_array(T)
 
@@ -212,6 +216,32 @@ def selection_fixture(name, spec, npiv):
             "sha256": gen.digest(T), "states": states}
 
 
+def phase1_fixture(name, spec):
+    """Simplex(tab) on an LP that needs artificial variables: the phase-1
+    pivots made by the constructor (simplex.py:36-108), the basis and size
+    it leaves, then solve() -- or the exception the reference raises."""
+    T, rows = source_of(spec)
+    t = ref_tableau_from_rows(rows)
+    log = []
+    fx = {"name": name, "mode": "phase1", **spec, "m": int(T.shape[0] - 1),
+          "n": int(T.shape[1] - 1), "sha256": gen.digest(T)}
+    try:
+        s = LoggingSimplex(t, log)
+        fx["init_seq"] = [[r, c] for r, c, _ in log]
+        fx["init_bfs"] = list(s.getBasicSequence())
+        fx["init_size"] = list(t.getTableauSize())
+        k0 = len(log)
+        s.solve()
+        fx["seq"] = [[r, c] for r, c, _ in log[k0:]]
+        fx["objective"] = fs(s.getObjValue())
+        fx["bfs"] = list(s.getBasicSequence())
+    except Exception as ex:                      # noqa: BLE001 -- recorded as the outcome
+        fx["error"] = type(ex).__name__
+        fx["message"] = str(ex)[:120]
+        fx["init_seq"] = [[r, c] for r, c, _ in log]
+    return fx
+
+
 def kat_fixture():
     """The reference's own known-answer pivot test (test_tableau.py:9-29,
     :220-227) recorded as exact values."""
@@ -234,7 +264,7 @@ def main():
     ap.add_argument("--big", action="store_true")
     args = ap.parse_args()
 
-    small = {"kat": [kat_fixture()], "solve": [], "standard_k": [], "selection": []}
+    small = {"kat": [kat_fixture()], "solve": [], "standard_k": [], "selection": [], "phase1": []}
     z, c, b, a = gen.beale_exact()
     small["solve"].append(solve_fixture("beale", {"exact": {"z": z, "c": c, "b": b, "a": a}}))
     for d in (3, 4, 5, 6, 8, 10):
@@ -269,6 +299,17 @@ def main():
         "sel_km_deg_d6", {"array": gen.klee_minty(6, True).tolist()}, 12))
     small["selection"].append(selection_fixture(
         "sel_beale", {"exact": {"z": z, "c": c, "b": b, "a": a}}, 12))
+    for kind in ("eq", "ge", "neg"):
+        for (m, ns) in ((4, 5), (6, 8), (10, 12), (16, 20)):
+            for seed in (1, 2, 3):
+                small["phase1"].append(phase1_fixture(
+                    f"p1_{kind}_{m}x{ns}_s{seed}",
+                    {"phase1": {"kind": kind, "m": m, "ns": ns, "seed": seed}}))
+    for seed in (1, 2):
+        small["phase1"].append(phase1_fixture(
+            f"p1_dep_6x8_s{seed}", {"phase1": {"kind": "dep", "m": 6, "ns": 8, "seed": seed}}))
+    small["phase1"].append(phase1_fixture(
+        "p1_infeasible_4", {"phase1": {"kind": "infeasible", "m": 2, "ns": 4, "seed": 0}}))
     with open(os.path.join(OUT, "small.json"), "w") as f:
         json.dump(small, f, separators=(",", ":"))
 

@@ -97,6 +97,24 @@ def test_exact_selection_rules_match_reference(fx):
         exact.pivot(T, *res)
 
 
+@pytest.mark.parametrize("fx", SMALL["selection"], ids=_ids(SMALL["selection"]))
+def test_f64_oracle_selection_rules_match_reference(fx):
+    """the float64 restatement's findPivotStandard/MinIndex/MaxIncrease/All at
+    every state of the reference's standard-rule walk"""
+    t = F64Tableau(fixture_input(fx))
+    for st in fx["states"]:
+        def norm(x):
+            return list(x) if isinstance(x, tuple) else x
+        assert norm(t.find(0)) == st["standard"]
+        assert norm(t.find(1)) == st["min_index"]
+        assert norm(t.find_max_increase()) == st["max_increase"]
+        assert [list(p) for p in t.find_all()] == st["all"]
+        res = t.find(0)
+        if isinstance(res, str):
+            break
+        t.pivot(*res)
+
+
 @pytest.mark.parametrize("fx", SMALL["solve"] + BIG["solve"], ids=_ids(SMALL["solve"] + BIG["solve"]))
 def test_f64_oracle_solve_matches_reference(fx):
     t = F64Tableau(fixture_input(fx))
@@ -137,3 +155,60 @@ def test_generator_is_counter_based():
     assert np.all(T[1:, 0] > 0) and np.all(T[0, 1:17] < 0)
     assert np.array_equal(T[1:, 17:], np.eye(16))
     assert np.all(np.abs(T * 64 - np.round(T * 64)) == 0)      # dyadic k/64
+
+
+@pytest.mark.parametrize("fx", SMALL["selection"], ids=_ids(SMALL["selection"]))
+def test_host_form_checks_match_reference(fx):
+    """the front-end's numpy predicates (lpsol_amd.Tableau host path) on the
+    float64 states of the reference's walk answer what the reference did"""
+    from lpsol_amd import Tableau
+    t = F64Tableau(fixture_input(fx))
+    for st in fx["states"]:
+        h = Tableau.fromArray(t.T)
+        bc = [-2] * t.m
+        assert h.isCanonical(bc) == st["is_canonical"]
+        if st["is_canonical"]:
+            assert bc == st["bcols"]
+        assert h.isOptimal() == st["is_optimal"]
+        assert h.isUnbounded() == st["is_unbounded"]
+        assert h.isInfeasible() == st["is_infeasible"]
+        assert h.isDegenerate() == st["is_degenerate"]
+        res = t.find(0)
+        if isinstance(res, str):
+            break
+        t.pivot(*res)
+
+
+@pytest.mark.parametrize("fx", SMALL["phase1"], ids=_ids(SMALL["phase1"]))
+def test_phase1_oracle_matches_reference(fx):
+    """oracle/phase1.py (Simplex._find_bfs on the float64 contract) against
+    the reference run on the same LP: every phase-1 pivot (artificial solve
+    and drive-out), the basis and size it leaves, then solve()."""
+    from oracle import phase1
+    o = phase1.solve_lp(fixture_input(fx))
+    assert o["init_seq"] == fx["init_seq"]
+    if fx.get("error") == "ValueError":              # infeasible: same exception
+        assert o.get("error") == "ValueError"
+        return
+    if fx.get("error") == "IndexError":
+        # the reference's _m bug (simplex.py:93) after dropping a dependent
+        # row; the restatement drops it and solves the LP without it
+        assert o["init_size"] == [fx["m"] - 1, fx["n"]]
+        twin = next(f for f in SMALL["phase1"] if f.get("phase1") == dict(fx["phase1"], kind="eq"))
+        obj = float(Fraction(twin["objective"]))
+        assert abs(o["objective"] - obj) <= REL * max(1.0, abs(obj))
+        return
+    assert o["init_bfs"] == fx["init_bfs"]
+    assert o["init_size"] == fx["init_size"]
+    assert o["seq"] == fx["seq"]
+    assert o["bfs"] == fx["bfs"]
+    obj = float(Fraction(fx["objective"]))
+    assert abs(o["objective"] - obj) <= REL * max(1.0, abs(obj))
+
+
+def test_phase1_golden_covers_every_outcome():
+    kinds = {fx["phase1"]["kind"] for fx in SMALL["phase1"]}
+    assert kinds == {"eq", "ge", "neg", "dep", "infeasible"}
+    assert {fx.get("error") for fx in SMALL["phase1"]} == {None, "IndexError", "ValueError"}
+    # phase 1 made drive-out pivots somewhere (artificial basic at value 0)
+    assert any(len(fx["init_seq"]) > 0 for fx in SMALL["phase1"] if fx["phase1"]["kind"] == "ge")
