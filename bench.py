@@ -52,8 +52,11 @@ def pivot_bytes(m: int, n: int) -> int:
     return 8 * (2 * (m + 1) * (n + 1) + (n + 1) + 2 * (m + 1))
 
 
+SWEEP_KERNEL = "k_sweep_st"
+
+
 def sweep_bytes(rows: int, n: int, block: int) -> int:
-    """Algorithmic bytes of one k_sweep launch on `rows` local rows applying
+    """Algorithmic bytes of one sweep (k_sweep_st) launch on `rows` local rows applying
     `block` deferred pivots: read and write every row once, read the block's
     pivot rows P and multiplier columns M."""
     return 8 * (2 * rows * (n + 1) + block * (n + 1) + block * rows)
@@ -109,13 +112,13 @@ def cpu_baseline(seconds_target: float = 15.0) -> dict:
 
 
 def load_traffic(path: str | None, block: int):
-    """HBM bytes per k_sweep launch measured by scripts/hbm_traffic.py (two
+    """HBM bytes per sweep launch measured by scripts/hbm_traffic.py (two
     rocprofv3 --pmc passes on this workload), or None if not measured for
-    this pivots-per-sweep setting."""
+    this kernel and pivots-per-sweep setting."""
     if path and os.path.exists(path):
         with open(path) as f:
             d = json.load(f)
-        if d.get("block") == block:
+        if d.get("block") == block and d.get("kernel", "").split("<")[0] == SWEEP_KERNEL:
             return d.get("hbm_bytes_per_launch")
     return None
 
@@ -293,7 +296,7 @@ def main():
         # once pivots are deferred -- that is the point of the sweep)
         "unblocked_equivalent_GBps": pivot_bytes(m, n) * lp_pps / 1e9,
         "roofline": {
-            "kernel": f"k_sweep (rank-{args.block} elimination, {args.block} deferred pivots)",
+            "kernel": f"{SWEEP_KERNEL} (rank-{args.block} elimination, {args.block} deferred pivots)",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,

@@ -89,17 +89,26 @@ for step in "$@"; do
             done ;;
         pmcsq)
             export TMPDIR=/tmp
-            for B in 16 32; do
+            for B in ${PMC_BLOCKS:-16 32}; do
                 run pmcsq_b$B 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_LDS --output-format csv -d "$OUT/pmcsq_b$B" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline --block $B
                 run pmcgr_b$B 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcgr_b$B" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline --block $B
             done ;;
+        st)
+            # strip sweep: full GPU suite on one variant, then timing
+            LPGPU_SWEEP=${ST_VARIANT:-21} run pytest_st 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 60 --timeout-method thread
+            for V in ${ST_BENCH:-0 21 23 24}; do
+                for B in 16 32; do
+                    LPGPU_SWEEP=$V run bench_st${V}_b$B 300 python bench.py --no-cpu-baseline --steps 1024 --block $B
+                done
+            done
+            grep -H -o '"avg_launch_us": [0-9.]*' "$OUT"/bench_st*.log ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
         pmc)
             export TMPDIR=/tmp
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
-            run pmc_json 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" --block 32
+            run pmc_json 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" --block 32 --kernel k_sweep_st
             # later steps of this call (bench) report it as roofline.traffic
             if [ -f "$OUT/hbm_traffic.json" ]; then cp "$OUT/hbm_traffic.json" profiles/r01/hbm_traffic.json; fi ;;
         proffinal)
