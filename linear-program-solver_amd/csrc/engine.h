@@ -122,7 +122,7 @@ struct Args {
     int pad;
     lp_tol tol;
     long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
-    unsigned long long *gran;  // k_group summaries: 2 phases x GROUP_MAXBLOCKS x 8 tagged granules
+    unsigned long long *gran;  // k_group summaries: 3 phases (ratio, row 0, XCD check) x GROUP_MAXBLOCKS x 8 tagged granules
     // pipelined groups (k_group only): the previous group's pivots are not yet
     // in T (its sweep runs concurrently); lag = 1 applies them on the fly first
     const double *Pp;    // previous group's P (BMAX x ld)
@@ -212,6 +212,26 @@ __host__ __device__ inline long long group_blocks(long long rc, long long ld, in
     if ((ld + g - 1) / g > 4 * GROUP_THREADS) return 0;   // more than 4 columns per lane
     if ((rc + g - 1) / g > GROUP_ROWS) return 0;          // more than one row per lane
     return group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX ? 0 : g;
+}
+// k_group workgroups when they are all to run on ONE XCD (cus = its CUs; on
+// unless LPGPU_SEL_XCD=0): at most GROUP_ROWS rows per block, at most 4
+// columns per lane, and every block co-resident on those CUs (LDS-bound).
+// 0 when the mode is off or the shape does not fit.
+inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *v = std::getenv("LPGPU_SEL_XCD");
+        on = v ? std::atoi(v) : 1;
+    }
+    if (!on || cus <= 0 || ld >= 0x7fffffffLL || rc >= 0x7fffffffLL) return 0;
+    long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
+    const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
+    if (g4 > g) g = g4;
+    if (g < 1) g = 1;
+    if (g > GROUP_MAXBLOCKS) return 0;
+    const long long per_cu = 160 * 1024 / (group_lds(rc, ld, g, count, 0) + 4096);   // + static LDS
+    return per_cu >= 1 && g <= per_cu * cus ? g : 0;
 }
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
 

@@ -315,7 +315,7 @@ static int alloc_handle(lp_handle *h)
     const size_t mbytes = 2 * ((size_t)lpk::BMAX * h->rows + lpk::M_PAD) * sizeof(double);
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
-    const size_t gbytes = 2 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
+    const size_t gbytes = 3 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
     HCHK(h, hipMalloc(&h->gran, gbytes));
     HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
     HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));

@@ -102,6 +102,26 @@ for step in "$@"; do
                 done
             done
             grep -H -o '"avg_launch_us": [0-9.]*' "$OUT"/bench_st*.log ;;
+        stvar)
+            for rep in 1 2; do
+                for V in ${ST_BENCH:-21 25 26 27}; do
+                    LPGPU_SWEEP=$V run bench_v${V}_$rep 300 python bench.py --no-cpu-baseline --steps 1024
+                done
+                for C in ${ST_BPC:-2 4}; do
+                    LPGPU_SWEEP_BPC=$C run bench_bpc${C}_$rep 300 python bench.py --no-cpu-baseline --steps 1024
+                done
+            done
+            grep -H -o '"avg_launch_us": [0-9.]*' "$OUT"/bench_v*.log "$OUT"/bench_bpc*.log | awk 'NR % 2 == 1' ;;
+        xcd)
+            # selection blocks on one XCD with L2-local hand-offs
+            LPGPU_SEL_XCD=1 run pytest_xcd 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 60 --timeout-method thread
+            for rep in 1 2; do
+                for X in 0 1; do
+                    LPGPU_SEL_XCD=$X run bench_x${X}_$rep 300 python bench.py --no-cpu-baseline --steps 1024
+                done
+            done
+            LPGPU_SEL_XCD=1 run stamps_x1 300 python scripts/diag_stamps.py
+            grep -H -o '"value": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_x*.log ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
         pmc)
