@@ -1433,9 +1433,11 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         if (li == R) ownpiv |= 1ull << t;
         if (tid == 0) sR[t] = R;
         double vmin = INFINITY, v0 = 0.0;
+        double vv[IPL];                   // new row 0 on own columns (INFINITY: not a variable column)
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             const long long j = jc0 + tid + k * nth;
+            vv[k] = INFINITY;
             if (j < jc1) {
                 const double p = pv_[k];
                 lP[kc[k] * cs + t] = p;
@@ -1444,72 +1446,45 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 l0[kc[k]] = v;
                 st_x(&A.row0[j], v, fast);
                 if (j == 0) v0 = v;
-                if (j >= 1 && j <= A.n) vmin = fmin(vmin, v);
+                if (j >= 1 && j <= A.n) {
+                    vmin = fmin(vmin, v);
+                    vv[k] = v;
+                }
             }
         }
         __syncthreads();
         stamp(A, b, t, 9);
-        // row-0 summary of own columns: columns j = jc0 + lane + 64k, so the
-        // first column with a property is the lowest lane of the first k
-        // whose ballot is non-empty
+        // row-0 summary of own columns, from registers: columns j = jc0 +
+        // lane + 64k, so the first column with a property is the lowest lane
+        // of the first k whose ballot is non-empty
         const double el = block_min(vmin, sd);
-        long long efn = NONE;
-        for (long long j0 = jc0; j0 < jc1 && efn == NONE; j0 += nth) {
-            const long long j = j0 + tid;
-            const bool ok = j < jc1 && j >= 1 && j <= A.n && l0[j - jc0] < -A.tol.cost;
-            const u64 mask = __ballot(ok);
-            if (mask) efn = j0 + __builtin_ctzll(mask);
-        }
-        long long ei = NONE;
+        long long efn = NONE, ei = NONE;
         double eq = 0.0;
-        if (el < INFINITY) {
-            const double ethr = tie_band(el, A.tol.cost_tie);
-            for (long long j0 = jc0; j0 < jc1; j0 += nth) {
-                const long long j = j0 + tid;
-                const double v = j < jc1 ? l0[j - jc0] : INFINITY;
-                const u64 mask = __ballot(j >= 1 && j <= A.n && v <= ethr);
-                if (mask) {
-                    const int f = __builtin_ctzll(mask);
-                    ei = j0 + f;
-                    eq = mk_d(__builtin_amdgcn_readlane(lo32(v), f), __builtin_amdgcn_readlane(hi32(v), f));
-                    break;
-                }
+        const double ethr = tie_band(el, A.tol.cost_tie);
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const u64 mn = __ballot(vv[k] < -A.tol.cost);
+            if (mn && efn == NONE) efn = jc0 + k * nth + __builtin_ctzll(mn);
+            const u64 mb = __ballot(el < INFINITY && vv[k] <= ethr);
+            if (mb && ei == NONE) {
+                const int f = __builtin_ctzll(mb);
+                ei = jc0 + k * nth + f;
+                eq = rl_d(lo32(vv[k]), hi32(vv[k]), f);
             }
         }
         stamp(A, b, t, 10);
-        if (b == 0 && tid == 0) {     // column 0 is in block 0's slice: v0 = new row0[0]
-            st_x(&A.dR[t], R, fast);
-            st_x(&A.dC[t], C, fast);
-            st_x(&ctl->r, rglob, fast);
-            if (npiv < A.logcap) {
-                A.log[2 * npiv] = rglob;
-                A.log[2 * npiv + 1] = C - 1;
-            }
-            st_x(&ctl->npiv, npiv + 1, fast);
-            st_x(&ctl->ndef[grp], (long long)(t + 1), fast);
-            if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
-                nstd += 1;
-                // stall bookkeeping (simplex.py:132-137), min-index switch (:123,138)
-                const double z = -v0;
-                if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) stuck += 1;
-                else stuck = 0;
-                if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
-                st_x(&ctl->nstd, nstd, fast);
-                st_x(&ctl->stuck, stuck, fast);
-                st_x(&ctl->rule, rule, fast);
-            }
+        // stall bookkeeping (simplex.py:132-137), min-index switch (:123,138)
+        // by block 0 (column 0 is in its slice: v0 = new row0[0]); the rule
+        // travels in its summary, the records are stored after the publish
+        if (b == 0 && tid == 0 && mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
+            nstd += 1;
+            const double z = -v0;
+            if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) stuck += 1;
+            else stuck = 0;
+            if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
         }
         rule = __builtin_amdgcn_readfirstlane(rule);   // block 0 lane 0 may have switched it
         const double p0n = b == 0 ? lP[t] : 0.0;       // P[t][0] (column 0 is block 0's first)
-        if (t == count - 1) {         // the next launch reads plain summaries
-            if (tid == 0) {
-                st_x(&A.erec[b].l, el, fast);
-                st_x(&A.erec[b].i, ei, fast);
-                st_x(&A.erec[b].q, eq, fast);
-                st_x(&A.erec[b].fneg, efn, fast);
-                if (b == 0) st_x(&A.erec[0].rule, (long long)rule, fast);
-            }
-        }
         {
             unsigned wv = 0;
             if (tid == 0) wv = lo32(el);
@@ -1521,6 +1496,30 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 6) wv = lo32(p0n);
             else if (tid == 7) wv = hi32(p0n);
             publish(&grE[b * 8], gtag(seq, t, 1), wv, NGE, fast);
+        }
+        // records read after the launch only (host, sweep, next launch)
+        if (b == 0 && tid == 0) {
+            st_x(&A.dR[t], R, fast);
+            st_x(&A.dC[t], C, fast);
+            st_x(&ctl->r, rglob, fast);
+            if (npiv < A.logcap) {
+                A.log[2 * npiv] = rglob;
+                A.log[2 * npiv + 1] = C - 1;
+            }
+            st_x(&ctl->npiv, npiv + 1, fast);
+            st_x(&ctl->ndef[grp], (long long)(t + 1), fast);
+            if (mode == MODE_SOLVE) {
+                st_x(&ctl->nstd, nstd, fast);
+                st_x(&ctl->stuck, stuck, fast);
+                st_x(&ctl->rule, (int)rule, fast);
+            }
+        }
+        if (t == count - 1 && tid == 0) {     // the next launch reads plain summaries
+            st_x(&A.erec[b].l, el, fast);
+            st_x(&A.erec[b].i, ei, fast);
+            st_x(&A.erec[b].q, eq, fast);
+            st_x(&A.erec[b].fneg, efn, fast);
+            if (b == 0) st_x(&A.erec[0].rule, (long long)rule, fast);
         }
         bstamp(A, b, t, 1);
         ++npiv;
@@ -2111,6 +2110,10 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
         if (nr <= 1) GROUP_LAUNCH(1, 2);
         else if (nr <= 2) GROUP_LAUNCH(2, 2);
         else GROUP_LAUNCH(NRMAX, 2);
+    } else if (ipl == 3 && nr <= 1) {   // one-XCD geometry of cfg3-like shapes (129 columns per block)
+        GROUP_LAUNCH(1, 3);
+    } else if (ipl == 3 && nr <= 2) {
+        GROUP_LAUNCH(2, 3);
     } else {
         if (nr <= 1) GROUP_LAUNCH(1, 4);
         else if (nr <= 2) GROUP_LAUNCH(2, 4);

@@ -122,6 +122,14 @@ for step in "$@"; do
             done
             LPGPU_SEL_XCD=1 run stamps_x1 300 python scripts/diag_stamps.py
             grep -H -o '"value": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_x*.log ;;
+        check)
+            # the default build: GPU suite, two timing runs, phase stamps
+            run pytest_check 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 60 --timeout-method thread
+            for rep in 1 2; do
+                run bench_c$rep 300 python bench.py --no-cpu-baseline --steps 1024
+            done
+            run stamps_c 300 python scripts/diag_stamps.py
+            grep -H -o '"value": [0-9.]*\|"us_per_pivot": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_c*.log ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
         pmc)
