@@ -165,14 +165,15 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 // one persistent launch selecting up to `count` chained pivots of a group;
 // seq numbers the launches of a handle (1 .. 2^24-1, then wraps to 1): it tags
 // the launch's summaries so no stale granule can match
-// xr: one rank of a row-sharded job.  As (device array of nshard Args): the
+// xr: one rank of a row-sharded job (2: its selection may run on one XCD).
+// As (device array of nshard Args): the
 // in-process shards of one device, all in this one launch
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
                         unsigned seq, int bmax, int lag_layout, int xr = 0,
                         const Args *As = nullptr, int nshard = 1);
 // row-sharded: every rank writes a tagged granule to every rank's buffer and
 // waits (bounded) for all of them; *ok = 1 if all arrived (peer exchange works)
-hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, int *ok_dev);
+hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev);
 int group_fits(const Args &A, int bmax, int lag_layout, int xr, int nshard);
 #ifndef LPK_GROUP_BLOCKS
 #define LPK_GROUP_BLOCKS 64

@@ -1789,20 +1789,26 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
 // into rank p's summary slot, then every lane waits for rank p's granule in
 // the local buffer (bounded)
-__global__ void k_peer_ping(Args A, unsigned tag, int *ok)
+// (every rank also sends its flag bits; *ok = 1 | OR of the ranks' flags << 1
+// when all arrived, 0 otherwise)
+__global__ void k_peer_ping(Args A, unsigned tag, unsigned flags, int *ok)
 {
     const int N = A.nranks, p = threadIdx.x;
-    if (p < N) st_sys(&A.peer[p][A.rank * 8], ((u64)tag << 32) | (unsigned)A.rank);
+    if (p < N) st_sys(&A.peer[p][A.rank * 8], ((u64)tag << 32) | (flags << 8) | (unsigned)A.rank);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool got = p >= N;
+    unsigned f = 0;
     while (!got) {
         const u64 v = ld_sys(&A.xbuf[p * 8]);
-        got = (unsigned)(v >> 32) == tag && (unsigned)v == (unsigned)p;
+        got = (unsigned)(v >> 32) == tag && ((unsigned)v & 0xffu) == (unsigned)p;
+        f = ((unsigned)v >> 8) & 0xffu;
         if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;   // 2 s
         __builtin_amdgcn_s_sleep(2);
     }
     const bool all = __all(got);
-    if (threadIdx.x == 0) *ok = all ? 1 : 0;
+    // OR of the flags over the lanes (ranks)
+    for (int o = 32; o >= 1; o >>= 1) f |= (unsigned)__shfl_xor((int)f, o);
+    if (threadIdx.x == 0) *ok = all ? (int)(1u | (f << 1)) : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2089,7 +2095,9 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
     // must match across ranks), sized for the largest row block
     const long long rcg = xr ? (A.m + A.nranks - 1) / A.nranks : A.rc;
     long long g = 0;
-    const int xmode = (!xr && !As && !lag_layout) ? group_blocks_xcd(rcg, A.ld, bmax, sweep_cus() / 8) : 0;
+    // one-XCD selection: single device, or a rank of a sharded job whose
+    // ranks all agreed to it (xr == 2: no two ranks share a GPU)
+    const int xmode = (xr != 1 && !As && !lag_layout) ? group_blocks_xcd(rcg, A.ld, bmax, sweep_cus() / 8) : 0;
     if (xmode) g = xmode;
     else g = group_blocks(rcg, A.ld, bmax, lag_layout);
     if (g == 0) return hipErrorInvalidValue;
@@ -2101,7 +2109,7 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
     do {                                                                                      \
         if (xr)                                                                               \
             hipLaunchKernelGGL((k_group<NRV, IPLV, true>), grid, dim3(GROUP_THREADS), lds, s, \
-                               A, As, (int)g, grp, count, from_erec, seq, bmax, 0);           \
+                               A, As, (int)g, grp, count, from_erec, seq, bmax, xmode ? 1 : 0); \
         else                                                                                  \
             hipLaunchKernelGGL((k_group<NRV, IPLV, false>), grid, dim3(GROUP_THREADS), lds, s, \
                                A, As, (int)g, grp, count, from_erec, seq, bmax, xmode ? 1 : 0); \
@@ -2164,10 +2172,10 @@ int group_fits(const Args &A, int bmax, int lag_layout, int xr, int nshard)
     return (long long)(per_cu - 1) * ncu >= g * nshard ? 1 : 0;
 }
 
-hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, int *ok_dev)
+hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev)
 {
-    if (A.nranks > NRANK_MAX || !A.xbuf || !A.peer) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_peer_ping, dim3(1), dim3(64), 0, s, A, tag, ok_dev);
+    if (A.nranks > NRANK_MAX || !A.xbuf || !A.peer || flags > 0xffu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_peer_ping, dim3(1), dim3(64), 0, s, A, tag, flags, ok_dev);
     return hipGetLastError();
 }
 

@@ -60,6 +60,7 @@ struct lp_handle {
     unsigned long long **dpeer = nullptr;   // device table: every rank's buffer
     std::vector<void *> ipc_open;           // peer buffers opened from IPC handles
     bool peer_ok = false;                   // the exchange is set up and validated
+    bool xr_xcd = false;                    // every rank on its own GPU: one-XCD selection
     bool peer_enable = true;                // LPGPU_PEER=0 keeps the RCCL per-pivot path
     hipStream_t sx = nullptr;               // in-process shards: own stream for the persistent launch
     // column scans / form checks (allocated on first use)
@@ -520,6 +521,7 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     if (!h || !h->comm || !h->xbuf) return h ? fail(h, LP_BAD_ARG, "lp_peer_handle first") : LP_BAD_ARG;
     HCHK(h, hipSetDevice(h->dev));
     std::vector<unsigned long long *> tab(h->nranks, nullptr);
+    bool shared = false;
     const char *all = static_cast<const char *>(handles);
     for (int p = 0; p < h->nranks; ++p) {
         if (p == h->rank) {
@@ -532,6 +534,10 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
         HCHK(h, hipIpcOpenMemHandle(&ptr, hd, hipIpcMemLazyEnablePeerAccess));
         h->ipc_open.push_back(ptr);
         tab[p] = static_cast<unsigned long long *>(ptr);
+        // a peer buffer on this very GPU: two ranks share it (tests)
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, ptr) != hipSuccess || at.device == h->dev) shared = true;
+        (void)hipGetLastError();
     }
     if (!h->dpeer) HCHK(h, hipMalloc(&h->dpeer, lpk::NRANK_MAX * sizeof(void *)));
     HCHK(h, hipMemcpy(h->dpeer, tab.data(), tab.size() * sizeof(void *), hipMemcpyHostToDevice));
@@ -540,7 +546,9 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     HCHK(h, hipMalloc(&dok, sizeof(int)));
     Args A = args_of(h);
     A.peer = h->dpeer;
-    const hipError_t e = lpk::launch_peer_ping(h->s, A, 7u, dok);
+    // the ping also tells every rank whether any two ranks share a GPU (their
+    // one-XCD selections could then not be resident together)
+    const hipError_t e = lpk::launch_peer_ping(h->s, A, 7u, shared ? 1u : 0u, dok);
     if (e == hipSuccess) (void)hipMemcpyAsync(&ok, dok, sizeof(int), hipMemcpyDeviceToHost, h->s);
     const hipError_t e2 = hipStreamSynchronize(h->s);
     (void)hipFree(dok);
@@ -550,6 +558,11 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     HCHK(h, hipDeviceSynchronize());
     if (!ok) return fail(h, LP_DEVICE_ERROR, "peer exchange check timed out");
     h->peer_ok = true;
+    h->xr_xcd = (ok & 2) == 0;
+    if (const char *v = std::getenv("LPGPU_XR_XCD")) {   // A/B and tests: 0 off, 2 even if shared
+        if (v[0] == '0') h->xr_xcd = false;
+        else if (v[0] == '2') h->xr_xcd = true;
+    }
     return LP_PIVOTED;
 }
 
@@ -792,7 +805,8 @@ static bool xr_ok(lp_handle *h)
 static int enqueue_xgroup(const Members &M, const std::vector<Args> &A, int grp, int cnt,
                           int from_erec)
 {
-    if (M.size() == 1) return launch_group_timed(M[0], M[0]->s, A[0], grp, cnt, from_erec, 0, 1);
+    if (M.size() == 1)
+        return launch_group_timed(M[0], M[0]->s, A[0], grp, cnt, from_erec, 0, M[0]->xr_xcd ? 2 : 1);
     lp_handle *h0 = M[0];
     auto g = std::dynamic_pointer_cast<GroupComm>(h0->comm);
     if (!g) return fail(h0, LP_DEVICE_ERROR, "multi-member launch without a shard group");

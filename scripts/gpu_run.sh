@@ -130,6 +130,14 @@ for step in "$@"; do
             done
             run stamps_c 300 python scripts/diag_stamps.py
             grep -H -o '"value": [0-9.]*\|"us_per_pivot": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_c*.log ;;
+        xrx)
+            # row-sharded selection on one XCD per rank, forced with two ranks on
+            # ONE GPU (their launches must then be resident together)
+            run pytest_peer 300 python -u -m pytest tests/test_gpu_peer_procs.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            LPGPU_XR_XCD=2 run pytest_peer_x 300 python -u -m pytest tests/test_gpu_peer_procs.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            run bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 256 --warmup 32 --no-rccl
+            LPGPU_XR_XCD=2 run bench_dist2_x 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 256 --warmup 32 --no-rccl
+            grep -H -o '"value": [0-9.]*\|"us_per_pivot": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_dist2*.log ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
         pmc)
