@@ -116,16 +116,32 @@ __device__ long long block_min_ll(long long v, long long *scratch)
 // (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH "Valid forms" row 1).
 // ---------------------------------------------------------------------------
 
+// Global-address-space views of device pointers: accesses through them are
+// global_* instructions.  A flat_* access (what a generic pointer loaded from
+// memory compiles to) also counts in lgkmcnt, so every later LDS wait would
+// wait for it too.  Only for pointers into device memory (never LDS).
+#define GAS __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ GAS T *gp(T *p)
+{
+    return (GAS T *)p;
+}
+template <typename T>
+__device__ __forceinline__ const GAS T *gp(const T *p)
+{
+    return (const GAS T *)p;
+}
+
 template <typename T>
 __device__ __forceinline__ void st_sc1(T *p, T v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T>
 __device__ __forceinline__ T ld_sc1(const T *p)
 {
-    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gp(const_cast<T *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -716,13 +732,13 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
 __device__ __forceinline__ void stamp(const Args &A, unsigned b, int t, int k)
 {
     if (A.stamps && b == 0 && threadIdx.x == 0 && t < BMAX)
-        A.stamps[t * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+        *gp(A.stamps + t * 16 + k) = (long long)__builtin_amdgcn_s_memrealtime();
 }
 // every block: when it published its ratio (k = 0) / row-0 (k = 1) summary
 __device__ __forceinline__ void bstamp(const Args &A, unsigned b, int t, int k)
 {
     if (A.stamps && threadIdx.x == 0 && t < BMAX)
-        A.stamps[BMAX * 16 + (b * BMAX + t) * 2 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+        *gp(A.stamps + BMAX * 16 + (b * BMAX + t) * 2 + k) = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 typedef unsigned long long u64;
@@ -756,7 +772,7 @@ __device__ __forceinline__ unsigned gtag(unsigned seq, int t, int ph)
 template <typename T>
 __device__ __forceinline__ void st_x(T *p, T v, bool fast)
 {
-    if (fast) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (fast) __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     else st_sc1(p, v);
 }
 
@@ -863,12 +879,12 @@ constexpr int CH = 8;    // deferred pivots applied per chunk (loads issued toge
 template <typename T>
 __device__ __forceinline__ void st_sys(T *p, T v)
 {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 template <typename T>
 __device__ __forceinline__ T ld_sys(const T *p)
 {
-    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(gp(const_cast<T *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // wall-clock bound of a cross-rank wait (the ranks' launches are enqueued by
 // different processes): 30 s of the 100 MHz real-time counter
@@ -940,8 +956,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     constexpr int nth = GROUP_THREADS;
     // this parity's previous sweep is complete (the host orders it); the
     // other parity holds the previous group, whose sweep may still be running
-    const int np = A.lag ? (int)ctl->ndef[grp ^ 1] : 0;
-    if (b == 0 && tid == 0) ctl->ndef[grp] = 0;
+    const int np = A.lag ? (int)*gp(&ctl->ndef[grp ^ 1]) : 0;
+    if (b == 0 && tid == 0) *gp(&ctl->ndef[grp]) = 0;
     if (ld_sc1(&ctl->status) != LP_PIVOTED) return;
     u64 *grR = A.gran;                         // ratio summaries [G][8]
     u64 *grE = A.gran + GROUP_MAXBLOCKS * 8;   // row-0 summaries [G][8]
@@ -986,26 +1002,26 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         pcol[k] = lP + kc[k] * cs;
         pcolp[k] = lPp + kc[k] * cs;
     }
-    for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = A.row0[j];
-    if (own) lc[tid] = A.col0[li];
+    for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = *gp(A.row0 + j);
+    if (own) lc[tid] = *gp(A.col0 + li);
     u64 ownpiv = 0, ownpivp = 0;             // pivots s whose pivot row is this lane's row
     for (int s = 0; s < np; ++s) {
-        if (own) mrowp[s] = A.Mp[mi(A.rows, li, s)];
-        for (long long j = jc0 + tid; j < jc1; j += nth) lPp[(j - jc0) * cs + s] = A.Pp[s * A.ld + j];
-        if (A.dRp[s] == li) ownpivp |= 1ull << s;
+        if (own) mrowp[s] = *gp(A.Mp + mi(A.rows, li, s));
+        for (long long j = jc0 + tid; j < jc1; j += nth) lPp[(j - jc0) * cs + s] = *gp(A.Pp + s * A.ld + j);
+        if (*gp(A.dRp + s) == li) ownpivp |= 1ull << s;
     }
-    if (tid < np) sRp[tid] = A.dRp[tid];
-    const long long cap = ctl->cap;
-    const int mode = ctl->mode;
+    if (tid < np) sRp[tid] = *gp(A.dRp + tid);
+    const long long cap = *gp(&ctl->cap);
+    const int mode = *gp(&ctl->mode);
     // counters live in registers for the launch (block 0 publishes them)
     long long npiv = ld_sc1(&ctl->npiv);
     int rule = ld_sc1(&ctl->rule);
     long long nstd = 0, stuck = 0;
     double z0 = 0.0;
     if (b == 0 && tid == 0) {
-        nstd = ctl->nstd;
-        stuck = ctl->stuck;
-        z0 = ctl->z0;
+        nstd = *gp(&ctl->nstd);
+        stuck = *gp(&ctl->stuck);
+        z0 = *gp(&ctl->z0);
     }
     int status = LP_PIVOTED;
     int pending = -1;                 // pivot whose column-0 update is still due
@@ -1102,9 +1118,9 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         stamp(A, b, t, 2);
         // ---- ratio test over own rows; M[t] of own rows.  The tableau column
         //      load is issued before the cross-block loads (one round trip).
-        double a = own ? A.T[li * A.ld + C] : 0.0;
+        double a = own ? *gp(A.T + li * A.ld + C) : 0.0;
         if (tid < t) sPc[tid] = ld_sc1(&A.P[tid * A.ld + C]);
-        if (tid < np) sPcp[tid] = A.Pp[tid * A.ld + C];
+        if (tid < np) sPcp[tid] = *gp(A.Pp + tid * A.ld + C);
         if (tid == 0) {
             if (b == 0) st_x(&ctl->c, C - 1, fast);
             if (C >= jc0 && C < jc1) st_x(&A.M[mi(A.rows, 0, t)], l0[C - jc0], fast);   // row 0's multiplier
@@ -1240,10 +1256,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
 #pragma unroll
             for (int k = 0; k < IPL; ++k) {
                 const long long j = jc0 + tid + k * nth;
-                xv[k] = j < jc1 ? A.T[Rl * A.ld + j] : 0.0;
+                xv[k] = j < jc1 ? *gp(A.T + Rl * A.ld + j) : 0.0;
             }
             if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, Rl, tid)]);
-            if (tid < np) sMrp[tid] = A.Mp[mi(A.rows, Rl, tid)];
+            if (tid < np) sMrp[tid] = *gp(A.Mp + mi(A.rows, Rl, tid));
             // pivots s whose pivot row is Rl: the select instead of the FMA (uniform)
             const u64 rpiv = __ballot(tid < t && sR[tid] == Rl);
             const u64 rpivp = __ballot(tid < np && sRp[tid] == Rl);
@@ -1274,10 +1290,18 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             };
             chain_row(np, sMrp, pcolp, rpivp);
             chain_row(t, sMr, pcol, rpiv);
+            if (A.stamps) {       // diagnostic: the chain's results exist
+                asm volatile("" ::"v"(xv[0]), "v"(xv[IPL - 1]));
+                stamp(A, b, t, 12);
+            }
 #pragma unroll
             for (int k = 0; k < IPL; ++k) {
                 const long long j = jc0 + tid + k * nth;
                 pv_[k] = (j == C) ? 1.0 : xv[k] / av;
+            }
+            if (A.stamps) {
+                asm volatile("" ::"v"(pv_[0]), "v"(pv_[IPL - 1]));
+                stamp(A, b, t, 13);
             }
             __syncthreads();      // sMr is reused
         };
@@ -1302,14 +1326,14 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 else if (tid == 5) wv = lo32(aR);
                 else wv = hi32(aR);
                 for (int p = 0; p < N; ++p)
-                    st_sys(&A.peer[p][par * XS_SUM_PAR + A.rank * 8 + tid], tg | wv);
+                    st_sys(&(*gp(A.peer + p))[par * XS_SUM_PAR + A.rank * 8 + tid], tg | wv);
             }
             // this rank's slot of pivot-row slices in every peer's buffer
             auto send_row = [&](int ph) {
                 const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
                 for (int p = 0; p < N; ++p) {
                     if (p == A.rank) continue;
-                    u64 *dst = A.peer[p] + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
+                    u64 *dst = (*gp(A.peer + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
                                (long long)b * XS_PROW_BLOCK;
 #pragma unroll
                     for (int k = 0; k < IPL; ++k) {
@@ -1380,7 +1404,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     if (b == 0 && tid < 3) {
                         const unsigned wv = tid == 0 ? (unsigned)((long long)r0w - 1 + A.rb) : tid == 1 ? a0 : a1;
                         for (int p = 0; p < N; ++p)
-                            st_sys(&A.peer[p][par * XS_SUM_PAR + NRANK_MAX * 8 + tid],
+                            st_sys(&(*gp(A.peer + p))[par * XS_SUM_PAR + NRANK_MAX * 8 + tid],
                                    ((u64)gtag(seq, t, 5) << 32) | wv);
                     }
                 }
@@ -1503,8 +1527,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             st_x(&A.dC[t], C, fast);
             st_x(&ctl->r, rglob, fast);
             if (npiv < A.logcap) {
-                A.log[2 * npiv] = rglob;
-                A.log[2 * npiv + 1] = C - 1;
+                *gp(A.log + 2 * npiv) = rglob;
+                *gp(A.log + 2 * npiv + 1) = C - 1;
             }
             st_x(&ctl->npiv, npiv + 1, fast);
             st_x(&ctl->ndef[grp], (long long)(t + 1), fast);
@@ -1794,7 +1818,7 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
 __global__ void k_peer_ping(Args A, unsigned tag, unsigned flags, int *ok)
 {
     const int N = A.nranks, p = threadIdx.x;
-    if (p < N) st_sys(&A.peer[p][A.rank * 8], ((u64)tag << 32) | (flags << 8) | (unsigned)A.rank);
+    if (p < N) st_sys(&(*gp(A.peer + p))[A.rank * 8], ((u64)tag << 32) | (flags << 8) | (unsigned)A.rank);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool got = p >= N;
     unsigned f = 0;

@@ -27,6 +27,10 @@ for t in range(15):
     print(t, " ".join(f"{n}={x:4.2f}" for n, x in zip(names, d)))
 avg = [sum(r[k] for r in rows[1:]) / (len(rows) - 1) for k in range(len(names))]
 print("avg", " ".join(f"{n}={x:4.2f}" for n, x in zip(names, avg)), "sum", round(sum(avg), 2))
+# pcomp split by stamps 12 (chain done) and 13 (division done): chain / div / store+row0
+sub = [[(buf[t * 16 + 12] - buf[t * 16 + 8]) / 100, (buf[t * 16 + 13] - buf[t * 16 + 12]) / 100,
+        (buf[t * 16 + 9] - buf[t * 16 + 13]) / 100] for t in range(1, 15)]
+print("pcomp split: chain=%.2f div=%.2f store=%.2f" % tuple(sum(x[i] for x in sub) / len(sub) for i in range(3)))
 
 # per-block publish times: spread across blocks and the last blocks
 G = 65
