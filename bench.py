@@ -18,9 +18,11 @@ of an 8192-variable tableau.
 ``value`` = pivots/s x N (each pivot sweeps N shards of 4096 x 8192), i.e.
 plain LP pivots/s at N = 1; ``lp_pivots_per_s`` is the LP-level rate.
 
-Inputs are resident in HBM before the timed region.  The rank-1 update
-kernel's launches inside the timed region are bracketed by HIP events on the
-engine's stream (lp_profile) for the roofline's achieved bandwidth.
+Inputs are resident in HBM before the timed region.  Every sweep and
+selection launch inside the timed region carries a pair of HIP events that
+the launch itself records at the kernel's start and end (hipExtLaunchKernelGGL
+on the engine's stream, lp_profile): the roofline's achieved bandwidth is the
+sweep's algorithmic bytes over that kernel time.
 """
 from __future__ import annotations
 

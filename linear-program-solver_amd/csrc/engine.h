@@ -161,7 +161,9 @@ hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
 // T_out <- A.T with the group's pivots (T_out == A.T: in place); nd_max >= ndef
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out);
+// (e0, e1: events recorded at the kernel's start and end, for lp_profile)
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out,
+                        hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // one persistent launch selecting up to `count` chained pivots of a group;
 // seq numbers the launches of a handle (1 .. 2^24-1, then wraps to 1): it tags
 // the launch's summaries so no stale granule can match
@@ -170,7 +172,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 // in-process shards of one device, all in this one launch
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
                         unsigned seq, int bmax, int lag_layout, int xr = 0,
-                        const Args *As = nullptr, int nshard = 1);
+                        const Args *As = nullptr, int nshard = 1, hipEvent_t e0 = nullptr,
+                        hipEvent_t e1 = nullptr);
 // row-sharded: every rank writes a tagged granule to every rank's buffer and
 // waits (bounded) for all of them; *ok = 1 if all arrived (peer exchange works)
 hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev);

@@ -33,6 +33,8 @@
 // aligned).
 #include "engine.h"
 
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 
 namespace lpk {
@@ -2061,7 +2063,8 @@ static int sweep_cus()
 // place; k_sweep for the pipelined mode's out-of-place sweeps.  LPGPU_SWEEP
 // selects another shape for A/B timing (20, 22, 23: k_sweep_st; 1: k_sweep),
 // LPGPU_SWEEP_BPC the strip sweep's workgroups per CU.
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out)
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out, hipEvent_t e0,
+                        hipEvent_t e1)
 {
     static int variant = -1, bpc = 0;
     if (variant < 0) {
@@ -2070,8 +2073,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
         if (const char *v = getenv("LPGPU_SWEEP_BPC")) bpc = atoi(v) > 0 ? atoi(v) : 0;
     }
 #define SWEEP_ST_ONE(W, RW, NBV, LA, SA)                                                     \
-    hipLaunchKernelGGL((k_sweep_st<W, RW, NBV, LA, SA>), grid, dim3(64 * W), 0, s, A.T, T_out, A.P, A.M, \
-                       A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
+    hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, LA, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, T_out, \
+                          A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
     /* as many row runs as fill the resident capacity (BPC workgroups per CU) */
 #define SWEEP_ST_LAUNCH(W, RW, BPC, LA, SA)                                                  \
     do {                                                                                     \
@@ -2091,9 +2094,9 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
     const int v = T_out != A.T ? 1 : variant;
     switch (v) {
     case 1:
-        hipLaunchKernelGGL((k_sweep<16, 4, true>),
-                           dim3((unsigned)((A.ld + 127) / 128), (unsigned)((A.rows + 63) / 64)),
-                           dim3(1024), 0, s, A.T, T_out, A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp);
+        hipExtLaunchKernelGGL((k_sweep<16, 4, true>),
+                              dim3((unsigned)((A.ld + 127) / 128), (unsigned)((A.rows + 63) / 64)),
+                              dim3(1024), 0, s, e0, e1, 0, A.T, T_out, A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp);
         break;
     case 20: SWEEP_ST_LAUNCH(16, 4, bpc ? bpc : 1, 0, 0); break;
     case 22: SWEEP_ST_LAUNCH(12, 4, bpc ? bpc : 2, 0, 0); break;
@@ -2109,7 +2112,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 }
 
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax, int lag_layout, int xr, const Args *As, int nshard)
+                        unsigned seq, int bmax, int lag_layout, int xr, const Args *As, int nshard,
+                        hipEvent_t e0, hipEvent_t e1)
 {
     if (xr && (lag_layout || A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
     if (count < 1 || count > bmax || bmax > BMAX || (A.lag && !lag_layout)) return hipErrorInvalidValue;
@@ -2132,10 +2136,10 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
 #define GROUP_LAUNCH(NRV, IPLV)                                                               \
     do {                                                                                      \
         if (xr)                                                                               \
-            hipLaunchKernelGGL((k_group<NRV, IPLV, true>), grid, dim3(GROUP_THREADS), lds, s, \
+            hipExtLaunchKernelGGL((k_group<NRV, IPLV, true>), grid, dim3(GROUP_THREADS), lds, s, e0, e1, 0, \
                                A, As, (int)g, grp, count, from_erec, seq, bmax, xmode ? 1 : 0); \
         else                                                                                  \
-            hipLaunchKernelGGL((k_group<NRV, IPLV, false>), grid, dim3(GROUP_THREADS), lds, s, \
+            hipExtLaunchKernelGGL((k_group<NRV, IPLV, false>), grid, dim3(GROUP_THREADS), lds, s, e0, e1, 0, \
                                A, As, (int)g, grp, count, from_erec, seq, bmax, xmode ? 1 : 0); \
     } while (0)
     if (ipl <= 2) {

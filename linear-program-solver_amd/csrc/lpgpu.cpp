@@ -740,8 +740,11 @@ static int ensure_log(lp_handle *h, int64_t need)
 }
 
 // event pair around a launch on stream st when profiling (kind 0 sweep, 1 selection)
-static int prof_begin(lp_handle *h, hipStream_t st)
+// the next pair of profiling events, recorded by the launch itself at the
+// kernel's start and end (hipExtLaunchKernelGGL): kernel time, no dispatch gap
+static int prof_slot(lp_handle *h, hipEvent_t *e0, hipEvent_t *e1, int kind)
 {
+    *e0 = *e1 = nullptr;
     if (!h->prof) return LP_PIVOTED;
     if (h->evused + 2 > h->ev.size()) {
         hipEvent_t a, b;
@@ -751,14 +754,8 @@ static int prof_begin(lp_handle *h, hipStream_t st)
         h->ev.push_back(b);
         h->evkind.push_back(0);
     }
-    HCHK(h, hipEventRecord(h->ev[h->evused], st));
-    return LP_PIVOTED;
-}
-
-static int prof_end(lp_handle *h, hipStream_t st, int kind)
-{
-    if (!h->prof) return LP_PIVOTED;
-    HCHK(h, hipEventRecord(h->ev[h->evused + 1], st));
+    *e0 = h->ev[h->evused];
+    *e1 = h->ev[h->evused + 1];
     h->evkind[h->evused / 2] = kind;
     h->evused += 2;
     return LP_PIVOTED;
@@ -769,9 +766,10 @@ static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, hipStream_t 
 {
     if (!st) st = h->s;
     if (!T_out) T_out = A.T;
-    CALL(prof_begin(h, st));
-    HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out));
-    return prof_end(h, st, 0);
+    hipEvent_t e0, e1;
+    CALL(prof_slot(h, &e0, &e1, 0));
+    HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out, e0, e1));
+    return LP_PIVOTED;
 }
 
 static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int grp, int cnt,
@@ -780,10 +778,11 @@ static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int g
 {
     // every rank of a sharded job advances gseq identically (same calls, same order)
     h->gseq = h->gseq % ((1u << 24) - 1) + 1;
-    CALL(prof_begin(h, st));
+    hipEvent_t e0, e1;
+    CALL(prof_slot(h, &e0, &e1, 1));
     HCHK(h, lpk::launch_group(st, A, grp, cnt, from_erec, h->gseq, h->block, lag_layout, xr, As,
-                              nshard));
-    return prof_end(h, st, 1);
+                              nshard, e0, e1));
+    return LP_PIVOTED;
 }
 
 static int pev_at(lp_handle *h, size_t k, hipEvent_t *e);
