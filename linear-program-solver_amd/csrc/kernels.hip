@@ -958,7 +958,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     constexpr int nth = GROUP_THREADS;
     // this parity's previous sweep is complete (the host orders it); the
     // other parity holds the previous group, whose sweep may still be running
-    const int np = A.lag ? (int)*gp(&ctl->ndef[grp ^ 1]) : 0;
+    const int np = __builtin_amdgcn_readfirstlane(A.lag ? (int)*gp(&ctl->ndef[grp ^ 1]) : 0);
     if (b == 0 && tid == 0) *gp(&ctl->ndef[grp]) = 0;
     if (ld_sc1(&ctl->status) != LP_PIVOTED) return;
     u64 *grR = A.gran;                         // ratio summaries [G][8]
@@ -1030,7 +1030,11 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     long long pendR = -1;
     double p0 = 0.0;                  // its P[.][0]
     __syncthreads();
-    for (int t = 0; t < count; ++t) {
+    for (int tv = 0; tv < count; ++tv) {
+        // the pivot index is wave-uniform; saying so keeps the chains'
+        // trip counts and bounds in SGPRs (scalar branches, no exec masking:
+        // the loop's exits look divergent to the compiler)
+        const int t = __builtin_amdgcn_readfirstlane(tv);
         stamp(A, b, t, 0);
         // ---- entering column
         long long C;
