@@ -75,7 +75,8 @@ int lp_create(int64_t m, int64_t n, int device, lp_handle **out);
  * objective) is replicated on every rank.  uid is the 128-byte RCCL unique id
  * from lp_comm_unique_id on rank 0, broadcast to all ranks by the caller;
  * uid NULL creates no RCCL communicator (the device-side peer exchange below
- * must then be set up: the per-pivot RCCL path is unavailable). */
+ * must then be set up, or the host's all-gather given with
+ * lp_set_host_allgather, for the per-pivot exchanges). */
 int lp_comm_unique_id(void *uid128);
 int lp_create_sharded(int64_t m, int64_t n, int device, int rank, int nranks,
                       const void *uid128, lp_handle **out);
@@ -104,6 +105,20 @@ int lp_shard_rows(const lp_handle *h, int64_t *row_begin, int64_t *row_count);
 int lp_peer_handle(lp_handle *h, void *handle);
 int lp_peer_open(lp_handle *h, const void *handles);
 int lp_peer_enable(lp_handle *h, int enable);
+
+/* The host's own all-gather for a multi-process sharded handle (gloo, MPI,
+ * ...): fn(ctx, send, recv, bytes) must gather `bytes` from every rank into
+ * recv in rank order (nranks * bytes) and return 0.  It combines the column
+ * scans' per-column results (lp_find_pivot_max_increase, lp_find_pivot_all,
+ * lp_form_checks; RCCL is used when this is not set) and, on a handle
+ * created without an RCCL communicator, carries the per-pivot exchanges of
+ * the per-pivot path (explicit and validated pivots, peer exchange disabled)
+ * synchronously.  No reference counterpart (the reference is one process);
+ * it replaces the collective the scans of simplex.py:286-360 and
+ * tableau.py:466-521 need once the rows are split across processes.
+ * LP_BAD_ARG on a handle that is not a multi-process shard. */
+typedef int (*lp_allgather_fn)(void *ctx, const void *send, void *recv, int64_t bytes);
+int lp_set_host_allgather(lp_handle *h, lp_allgather_fn fn, void *ctx);
 
 int lp_destroy(lp_handle *h);
 
@@ -148,19 +163,22 @@ int lp_run(lp_handle *h, int rule, int64_t k, int64_t *done);
  * the largest objective increase -c_j * (min ratio of column j); ties to the
  * first column, its ratio-test row.  LP_UNBOUNDED if any such column has no
  * eligible row (the reference returns at the first one, :319-320),
- * LP_OPTIMAL if no column qualifies; performs the pivot if do_pivot.  Not on
- * multi-process sharded handles (LP_BAD_ARG). */
+ * LP_OPTIMAL if no column qualifies; performs the pivot if do_pivot.  On a
+ * multi-process sharded handle every rank calls it (collective: the ranks'
+ * per-column results are all-gathered, see lp_set_host_allgather). */
 int lp_find_pivot_max_increase(lp_handle *h, int do_pivot, int64_t *r, int64_t *c);
 
 /* findPivotAll (simplex.py:330-360): every min-ratio pivot of every column,
- * column-major, rows in order; writes up to cap (r, c) pairs, *count = all. */
+ * column-major, rows in order; writes up to cap (r, c) pairs, *count = all.
+ * Collective on a multi-process sharded handle (every rank gets all pairs). */
 int lp_find_pivot_all(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count);
 
 /* Form checks of the current tableau, exact comparisons of the float64 values
  * (tableau.py:466-521): flags[0] isCanonical, [1] isOptimal, [2] isUnbounded,
  * [3] isInfeasible, [4] isDegenerate.  bcols (m entries, may be NULL) gets
  * isCanonical's basic column per row (-1: none) unless some b_i < 0, where
- * the reference leaves it untouched. */
+ * the reference leaves it untouched.  Collective on a multi-process sharded
+ * handle. */
 int lp_form_checks(lp_handle *h, int32_t *flags, int64_t *bcols);
 
 /* Pivot log of the last lp_solve / lp_run: (r, c) pairs, oldest first.  The

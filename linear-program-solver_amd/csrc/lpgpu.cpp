@@ -137,25 +137,75 @@ struct Comm {
     virtual int allgather(const Members &M) = 0;       // xs -> xr
 };
 
+// One process per rank.  The per-pivot exchanges use the RCCL communicator
+// when there is one; a handle created without a unique id (or whose peers
+// share a GPU, which RCCL refuses) can instead be given the host's own
+// all-gather (lp_set_host_allgather: gloo, MPI, ...), which the per-pivot
+// path then calls synchronously through pinned staging buffers.
 struct RcclComm : Comm {
-    ncclComm_t comm = nullptr;      // null: peer exchange only (no RCCL communicator)
+    ncclComm_t comm = nullptr;      // null: peer exchange / host collective only
+    lp_allgather_fn host_fn = nullptr;
+    void *host_ctx = nullptr;
+    std::vector<unsigned char> hs, hr;   // staging for host_fn
     ~RcclComm() override
     {
         if (comm) ncclCommDestroy(comm);
     }
     Members members(lp_handle *h) override { return Members{h}; }
+    // all-gather of `bytes` host bytes per rank into recv (rank order)
+    int gather_host(lp_handle *h, const void *send, void *recv, size_t bytes)
+    {
+        if (host_fn) {
+            if (host_fn(host_ctx, send, recv, (int64_t)bytes) != 0)
+                return fail(h, LP_DEVICE_ERROR, "host all-gather failed");
+            return LP_PIVOTED;
+        }
+        if (!comm) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator and no host all-gather");
+        unsigned char *d = nullptr;
+        HCHK(h, hipMalloc(&d, bytes * (h->nranks + 1)));
+        int st = LP_PIVOTED;
+        if (hipMemcpyAsync(d, send, bytes, hipMemcpyHostToDevice, h->s) != hipSuccess ||
+            ncclAllGather(d, d + bytes, bytes, ncclUint8, comm, h->s) != ncclSuccess ||
+            hipMemcpyAsync(recv, d + bytes, bytes * h->nranks, hipMemcpyDeviceToHost, h->s) != hipSuccess ||
+            hipStreamSynchronize(h->s) != hipSuccess)
+            st = fail(h, LP_DEVICE_ERROR, "RCCL all-gather of column statistics failed");
+        (void)hipFree(d);
+        return st;
+    }
     int allreduce_min(const Members &M) override
     {
         lp_handle *h = M[0];
-        if (!comm) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator (created without a unique id)");
-        NCHK(h, ncclAllReduce(h->xg, h->xg, 1, ncclFloat64, ncclMin, comm, h->s));
+        if (comm) {
+            NCHK(h, ncclAllReduce(h->xg, h->xg, 1, ncclFloat64, ncclMin, comm, h->s));
+            return LP_PIVOTED;
+        }
+        if (!host_fn) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator and no host all-gather");
+        double v = 0.0;
+        std::vector<double> all(h->nranks);
+        HCHK(h, hipMemcpyAsync(&v, h->xg, sizeof(double), hipMemcpyDeviceToHost, h->s));
+        HCHK(h, hipStreamSynchronize(h->s));
+        CALL(gather_host(h, &v, all.data(), sizeof(double)));
+        for (double x : all) v = std::min(v, x);
+        HCHK(h, hipMemcpyAsync(h->xg, &v, sizeof(double), hipMemcpyHostToDevice, h->s));
+        HCHK(h, hipStreamSynchronize(h->s));
         return LP_PIVOTED;
     }
     int allgather(const Members &M) override
     {
         lp_handle *h = M[0];
-        if (!comm) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator (created without a unique id)");
-        NCHK(h, ncclAllGather(h->xs, h->xr, (size_t)slot_len(h), ncclFloat64, comm, h->s));
+        const size_t bytes = (size_t)slot_len(h) * sizeof(double);
+        if (comm) {
+            NCHK(h, ncclAllGather(h->xs, h->xr, (size_t)slot_len(h), ncclFloat64, comm, h->s));
+            return LP_PIVOTED;
+        }
+        if (!host_fn) return fail(h, LP_DEVICE_ERROR, "no RCCL communicator and no host all-gather");
+        hs.resize(bytes);
+        hr.resize(bytes * h->nranks);
+        HCHK(h, hipMemcpyAsync(hs.data(), h->xs, bytes, hipMemcpyDeviceToHost, h->s));
+        HCHK(h, hipStreamSynchronize(h->s));
+        CALL(gather_host(h, hs.data(), hr.data(), bytes));
+        HCHK(h, hipMemcpyAsync(h->xr, hr.data(), hr.size(), hipMemcpyHostToDevice, h->s));
+        HCHK(h, hipStreamSynchronize(h->s));
         return LP_PIVOTED;
     }
 };
@@ -199,6 +249,15 @@ struct GroupComm : Comm {
 };
 
 static Members members_of(lp_handle *h) { return h->comm ? h->comm->members(h) : Members{h}; }
+
+// a multi-process shard: the scans combine every rank's per-column results
+// through an all-gather (RcclComm::gather_host)
+static RcclComm *multi_process(lp_handle *h)
+{
+    if (!h->comm || h->nranks <= 1) return nullptr;
+    return dynamic_cast<RcclComm *>(h->comm.get());
+}
+
 
 // ---------------------------------------------------------------------------
 // creation
@@ -573,6 +632,15 @@ extern "C" int lp_peer_enable(lp_handle *h, int enable)
             if (enable && !x->dpeer) return fail(h, LP_BAD_ARG, "no peer exchange set up");
             x->peer_ok = enable != 0;
         }
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_set_host_allgather(lp_handle *h, lp_allgather_fn fn, void *ctx)
+{
+    RcclComm *rc = multi_process(h);
+    if (!rc) return fail(h, LP_BAD_ARG, "not a multi-process sharded handle");
+    rc->host_fn = fn;
+    rc->host_ctx = ctx;
     return LP_PIVOTED;
 }
 
@@ -1163,15 +1231,14 @@ extern "C" int lp_pivot_checked(lp_handle *h, int64_t r, int64_t c)
 // ---------------------------------------------------------------------------
 // column scans: findPivotMaxIncrease, findPivotAll, form checks.  The stored
 // tableau is current at every API boundary (each call sweeps its pending
-// pivots).  Shards of one process are combined on the host in rank order; a
-// multi-process sharded handle would need a collective here (not provided).
+// pivots).  Per-column results of every shard are combined on the host in
+// rank order: the shards of one process directly, a multi-process job's
+// through one all-gather per pass (RCCL, or the host's own collective).
 // ---------------------------------------------------------------------------
 
 static int scan_members(lp_handle *h, Members &M)
 {
     M = members_of(h);
-    if (h->comm && M.size() == 1 && h->nranks > 1)
-        return fail(h, LP_BAD_ARG, "column scans are not available on a multi-process sharded handle");
     for (lp_handle *x : M) {
         HCHK(x, hipSetDevice(x->dev));
         if (!x->eager_ok) {                  // row 0 / column 0 mirrors after an upload
@@ -1190,6 +1257,24 @@ static int scan_members(lp_handle *h, Members &M)
     return LP_PIVOTED;
 }
 
+// the scan results of every shard in rank order: the in-process members, or
+// this process's shard and its peers' through the all-gather
+template <class T>
+static int gather_parts(lp_handle *h, const std::vector<T> &mine, std::vector<std::vector<T>> &parts)
+{
+    RcclComm *rc = multi_process(h);
+    if (!rc) {
+        parts.push_back(mine);
+        return LP_PIVOTED;
+    }
+    std::vector<T> all(mine.size() * h->nranks);
+    CALL(rc->gather_host(h, mine.data(), all.data(), mine.size() * sizeof(T)));
+    parts.clear();
+    for (int k = 0; k < h->nranks; ++k)
+        parts.emplace_back(all.begin() + k * mine.size(), all.begin() + (k + 1) * mine.size());
+    return LP_PIVOTED;
+}
+
 // per-column statistics over every shard, and the current row 0
 static int column_stats(lp_handle *h, const Members &M, std::vector<lpk::ColStat> &cs,
                         std::vector<double> &row0)
@@ -1197,20 +1282,22 @@ static int column_stats(lp_handle *h, const Members &M, std::vector<lpk::ColStat
     row0.assign(h->ld, 0.0);
     HCHK(h, hipMemcpyAsync(row0.data(), M[0]->row0, h->ld * sizeof(double), hipMemcpyDeviceToHost,
                            M[0]->s));
+    std::vector<std::vector<lpk::ColStat>> parts;
     std::vector<lpk::ColStat> part(h->ld);
-    for (size_t k = 0; k < M.size(); ++k) {
-        lp_handle *x = M[k];
+    for (lp_handle *x : M) {
         HCHK(x, lpk::launch_colstat(x->s, args_of(x), x->cstat));
         HCHK(x, hipMemcpyAsync(part.data(), x->cstat, x->ld * sizeof(lpk::ColStat),
                                hipMemcpyDeviceToHost, x->s));
         HCHK(x, hipStreamSynchronize(x->s));
-        if (k == 0) {
-            cs = part;
-            continue;
-        }
+        std::vector<std::vector<lpk::ColStat>> p;
+        CALL(gather_parts(x, part, p));
+        for (auto &q : p) parts.push_back(std::move(q));
+    }
+    cs = parts[0];
+    for (size_t k = 1; k < parts.size(); ++k)
         for (int64_t j = 0; j < h->ld; ++j) {
             lpk::ColStat &c = cs[j];
-            const lpk::ColStat &d = part[j];
+            const lpk::ColStat &d = parts[k][j];
             c.gmin = std::min(c.gmin, d.gmin);
             c.npos += d.npos;
             c.npos0 += d.npos0;
@@ -1219,28 +1306,32 @@ static int column_stats(lp_handle *h, const Members &M, std::vector<lpk::ColStat
             c.none += d.none;
             c.one_row = std::min(c.one_row, d.one_row);
         }
-    }
     return LP_PIVOTED;
 }
 
 // rows inside the band thr[j] of every shard: first[j] (global, first shard
-// in rank order that has one) and per-shard counts
+// in rank order that has one) and per-shard counts (every shard of the job,
+// rank order)
 static int band_pass(lp_handle *h, const Members &M, const std::vector<double> &thr,
                      std::vector<long long> &first, std::vector<std::vector<long long>> &counts)
 {
     first.assign(h->ld, lpk::NONE);
-    counts.assign(M.size(), std::vector<long long>(h->ld, 0));
-    std::vector<long long> f(h->ld);
-    for (size_t k = 0; k < M.size(); ++k) {
-        lp_handle *x = M[k];
+    counts.clear();
+    std::vector<long long> fc(2 * h->ld);
+    for (lp_handle *x : M) {
         HCHK(x, hipMemcpyAsync(x->cthr, thr.data(), x->ld * sizeof(double), hipMemcpyHostToDevice, x->s));
         HCHK(x, lpk::launch_colband(x->s, args_of(x), x->cthr, x->cfirst, x->ccount, nullptr, nullptr));
-        HCHK(x, hipMemcpyAsync(f.data(), x->cfirst, x->ld * sizeof(long long), hipMemcpyDeviceToHost, x->s));
-        HCHK(x, hipMemcpyAsync(counts[k].data(), x->ccount, x->ld * sizeof(long long),
+        HCHK(x, hipMemcpyAsync(fc.data(), x->cfirst, x->ld * sizeof(long long), hipMemcpyDeviceToHost, x->s));
+        HCHK(x, hipMemcpyAsync(fc.data() + x->ld, x->ccount, x->ld * sizeof(long long),
                                hipMemcpyDeviceToHost, x->s));
         HCHK(x, hipStreamSynchronize(x->s));
-        for (int64_t j = 0; j < h->ld; ++j)
-            if (first[j] == lpk::NONE) first[j] = f[j];
+        std::vector<std::vector<long long>> p;
+        CALL(gather_parts(x, fc, p));
+        for (auto &q : p) {
+            for (int64_t j = 0; j < h->ld; ++j)
+                if (first[j] == lpk::NONE) first[j] = q[j];
+            counts.emplace_back(q.begin() + h->ld, q.end());
+        }
     }
     return LP_PIVOTED;
 }
@@ -1300,10 +1391,11 @@ extern "C" int lp_find_pivot_all(lp_handle *h, int64_t *rc, int64_t cap, int64_t
     std::vector<std::vector<long long>> counts;
     CALL(band_pass(h, M, thr, first, counts));
     // column-major, shards (= rows) in order within a column
-    std::vector<std::vector<long long>> offs(M.size(), std::vector<long long>(h->ld, 0));
+    const size_t S = counts.size();                 // shards of the whole job
+    std::vector<std::vector<long long>> offs(S, std::vector<long long>(h->ld, 0));
     long long total = 0;
     for (int64_t j = 1; j <= h->n; ++j)
-        for (size_t k = 0; k < M.size(); ++k) {
+        for (size_t k = 0; k < S; ++k) {
             offs[k][j] = total;
             total += counts[k][j];
         }
@@ -1311,18 +1403,39 @@ extern "C" int lp_find_pivot_all(lp_handle *h, int64_t *rc, int64_t cap, int64_t
     if (total == 0 || cap <= 0) return LP_PIVOTED;
     long long *pairs = nullptr;
     HCHK(h, hipMalloc(&pairs, (size_t)total * 2 * sizeof(long long)));
-    for (size_t k = 0; k < M.size(); ++k) {
+    int st = LP_PIVOTED;
+    RcclComm *mp = multi_process(h);
+    for (size_t k = 0; k < M.size() && st == LP_PIVOTED; ++k) {
         lp_handle *x = M[k];
-        HCHK(x, hipMemcpyAsync(x->cthr, thr.data(), x->ld * sizeof(double), hipMemcpyHostToDevice, x->s));
-        HCHK(x, hipMemcpyAsync(x->coffs, offs[k].data(), x->ld * sizeof(long long),
-                               hipMemcpyHostToDevice, x->s));
-        HCHK(x, lpk::launch_colband(x->s, args_of(x), x->cthr, x->cfirst, x->ccount, x->coffs, pairs));
-        HCHK(x, hipStreamSynchronize(x->s));
+        const size_t ks = mp ? (size_t)x->rank : k;
+        if (hipMemcpyAsync(x->cthr, thr.data(), x->ld * sizeof(double), hipMemcpyHostToDevice, x->s) !=
+                hipSuccess ||
+            hipMemcpyAsync(x->coffs, offs[ks].data(), x->ld * sizeof(long long), hipMemcpyHostToDevice,
+                           x->s) != hipSuccess ||
+            lpk::launch_colband(x->s, args_of(x), x->cthr, x->cfirst, x->ccount, x->coffs, pairs) !=
+                hipSuccess ||
+            hipStreamSynchronize(x->s) != hipSuccess)
+            st = fail(h, LP_DEVICE_ERROR, "find-all pair pass failed");
+    }
+    std::vector<long long> mine((size_t)total * 2);
+    if (st == LP_PIVOTED &&
+        hipMemcpy(mine.data(), pairs, mine.size() * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+        st = fail(h, LP_DEVICE_ERROR, "find-all readback failed");
+    (void)hipFree(pairs);
+    if (st != LP_PIVOTED) return st;
+    if (mp) {
+        // every rank wrote only its own slots: take each slot from its owner
+        std::vector<std::vector<long long>> p;
+        CALL(gather_parts(h, mine, p));
+        for (int64_t j = 1; j <= h->n; ++j)
+            for (size_t k = 0; k < S; ++k)
+                for (long long q = offs[k][j]; q < offs[k][j] + counts[k][j]; ++q) {
+                    mine[2 * q] = p[k][2 * q];
+                    mine[2 * q + 1] = p[k][2 * q + 1];
+                }
     }
     const long long keep = std::min<long long>(total, cap);
-    const hipError_t e = hipMemcpy(rc, pairs, (size_t)keep * 2 * sizeof(long long), hipMemcpyDeviceToHost);
-    (void)hipFree(pairs);
-    HCHK(h, e);
+    std::memcpy(rc, mine.data(), (size_t)keep * 2 * sizeof(long long));
     return LP_PIVOTED;
 }
 
@@ -1340,7 +1453,11 @@ extern "C" int lp_form_checks(lp_handle *h, int32_t *flags, int64_t *bcols)
         HCHK(x, lpk::launch_rowpos(x->s, args_of(x), x->rowflag));
         HCHK(x, hipMemcpyAsync(rf.data(), x->rowflag, x->rc * sizeof(int), hipMemcpyDeviceToHost, x->s));
         HCHK(x, hipStreamSynchronize(x->s));
-        for (int64_t i = 0; i < x->rc; ++i) infeasible |= rf[i];
+        int any = 0;
+        for (int64_t i = 0; i < x->rc; ++i) any |= rf[i];
+        std::vector<std::vector<int>> p;
+        CALL(gather_parts(x, std::vector<int>{any}, p));
+        for (auto &q : p) infeasible |= q[0];
     }
     // isCanonical (tableau.py:466-496): b >= 0, then per row the first column
     // with zero reduced cost that is a unit vector with its 1 there

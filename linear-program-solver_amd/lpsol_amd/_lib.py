@@ -78,6 +78,7 @@ _PROTOS = {
     "lp_peer_handle": (C.c_int, [_H, C.c_char_p]),
     "lp_peer_open": (C.c_int, [_H, C.c_char_p]),
     "lp_peer_enable": (C.c_int, [_H, C.c_int]),
+    "lp_set_host_allgather": (C.c_int, [_H, C.c_void_p, C.c_void_p]),
     "lp_last_error": (C.c_char_p, [_H]),
 }
 
@@ -327,11 +328,48 @@ class Engine:
     def peer_enable(self, enable: bool):
         self._check(self.lib.lp_peer_enable(self.h, 1 if enable else 0), self.h)
 
+    def set_host_allgather(self, fn):
+        """Give a multi-process shard the host's all-gather: fn(bytes) -> list
+        of every rank's bytes in rank order (e.g. torch.distributed over gloo,
+        see gloo_allgather).  The column scans combine through it; a handle
+        without an RCCL communicator also runs its per-pivot exchanges
+        through it."""
+        def tramp(ctx, send, recv, nbytes):
+            try:
+                parts = fn(C.string_at(send, nbytes))
+                blob = b"".join(parts)
+                if len(blob) != nbytes * len(parts):
+                    return 1
+                C.memmove(recv, blob, len(blob))
+                return 0
+            except Exception:       # noqa: BLE001 - no exception may cross the C ABI
+                return 1
+        cb = _ALLGATHER_FN(tramp)
+        self._check(self.lib.lp_set_host_allgather(self.h, C.cast(cb, C.c_void_p), None), self.h)
+        self._allgather_cb = cb     # the library holds the pointer: keep it alive
+
     def select_time(self):
         """-> (total ms, launches) of the pivot-selection kernel since profile()."""
         ms, n = C.c_double(), C.c_int64()
         self.lib.lp_select_time(self.h, C.byref(ms), C.byref(n))
         return ms.value, n.value
+
+
+_ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+
+
+def gloo_allgather(group=None):
+    """A host all-gather over torch.distributed (CPU tensors: gloo) for
+    Engine.set_host_allgather."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(data: bytes) -> list[bytes]:
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(out, t, group=group)
+        return [o.numpy().tobytes() for o in out]
+    return fn
 
 
 def create_group(m: int, n: int, nshards: int, device: int = 0) -> list[Engine]:

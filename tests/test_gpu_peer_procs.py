@@ -18,12 +18,15 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,m,ns,k,block,tie", [
-    ("mixed", 200, 150, 60, 8, 1e-12),
-    ("tall", 300, 40, 50, 32, 1e-12),
-    ("mixed", 48, 32, 40, 4, 0.25),       # wide tie band: straddles across ranks
+@pytest.mark.parametrize("kind,m,ns,k,block,tie,mode", [
+    ("mixed", 200, 150, 60, 8, 1e-12, "peer"),
+    ("tall", 300, 40, 50, 32, 1e-12, "peer"),
+    ("mixed", 48, 32, 40, 4, 0.25, "peer"),       # wide tie band: straddles across ranks
+    ("mixed", 120, 90, 20, 8, 1e-12, "scan"),     # + column scans, explicit pivots (host all-gather)
+    ("pos", 64, 64, 10, 4, 1e-12, "scan"),
+    ("mixed", 60, 50, 30, 8, 1e-12, "host"),      # every exchange through the host all-gather
 ])
-def test_two_process_peer_exchange(kind, m, ns, k, block, tie):
+def test_two_process_peer_exchange(kind, m, ns, k, block, tie, mode):
     port = _free_port()
     procs = []
     for rank in range(2):
@@ -31,7 +34,7 @@ def test_two_process_peer_exchange(kind, m, ns, k, block, tie):
                    WORLD_SIZE="2", LOCAL_RANK="0")
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(HERE, "_peer_worker.py"), kind, str(m), str(ns), str(k),
-             str(block), str(tie)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+             str(block), str(tie), mode], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
     for p in procs:
         try:
