@@ -71,7 +71,9 @@ struct Ctl {
     unsigned pad;
     unsigned bar[2];     // grid-barrier counters of k_group (by group parity)
     unsigned bar_timeout;// set if a k_group barrier gave up (never expected)
-    unsigned pad2;
+    unsigned sel_xcc;    // XCD of the last one-XCD k_group launch (0xff: spread); a
+                         // pipelined sweep beside the next selection keeps off it
+    unsigned long long tiles[2];  // pipelined sweep: next tile (by group parity; k_group zeroes it)
 };
 
 // Per-block ratio-test summary.
@@ -221,7 +223,7 @@ __host__ __device__ inline long long group_blocks(long long rc, long long ld, in
 // unless LPGPU_SEL_XCD=0): at most GROUP_ROWS rows per block, at most 4
 // columns per lane, and every block co-resident on those CUs (LDS-bound).
 // 0 when the mode is off or the shape does not fit.
-inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus)
+inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus, int lag = 0)
 {
     static int on = -1;
     if (on < 0) {
@@ -234,9 +236,11 @@ inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus
     if (g4 > g) g = g4;
     if (g < 1) g = 1;
     if (g > GROUP_MAXBLOCKS) return 0;
-    const long long per_cu = 160 * 1024 / (group_lds(rc, ld, g, count, 0) + 4096);   // + static LDS
+    const long long per_cu = 160 * 1024 / (group_lds(rc, ld, g, count, lag) + 4096);   // + static LDS
     return per_cu >= 1 && g <= per_cu * cus ? g : 0;
 }
+// group_blocks_xcd for this device (0: the shape does not fit one XCD)
+long long group_blocks_xcd_here(long long rc, long long ld, int count, int lag);
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
 
 // per-column statistics of the local constraint rows (row 0 excluded)

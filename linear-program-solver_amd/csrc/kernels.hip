@@ -980,7 +980,12 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         for (int k = 0; k < NRMAX; ++k)
             if (threadIdx.x + k * GROUP_THREADS < G) same = same && wx[k][0] == xcc;
         fast = __all(same);
+        if (b == 0 && threadIdx.x == 0) *gp(&ctl->sel_xcc) = fast ? xcc : 0xffu;
+    } else if (b == 0 && threadIdx.x == 0) {
+        *gp(&ctl->sel_xcc) = 0xffu;
     }
+    // this parity's pipelined sweep (after this launch) starts at tile 0
+    if (b == 0 && threadIdx.x == 0) *gp(&ctl->tiles[grp]) = 0ull;
     const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= nth)
     const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
     const long long cpb = (A.ld + G - 1) / G;               // columns per block (<= IPL nth)
@@ -1007,10 +1012,29 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = *gp(A.row0 + j);
     if (own) lc[tid] = *gp(A.col0 + li);
     u64 ownpiv = 0, ownpivp = 0;             // pivots s whose pivot row is this lane's row
-    for (int s = 0; s < np; ++s) {
-        if (own) mrowp[s] = *gp(A.Mp + mi(A.rows, li, s));
-        for (long long j = jc0 + tid; j < jc1; j += nth) lPp[(j - jc0) * cs + s] = *gp(A.Pp + s * A.ld + j);
-        if (*gp(A.dRp + s) == li) ownpivp |= 1ull << s;
+    // the lagging group's multipliers of the own row and pivot-row values of
+    // the own columns, CH pivots per round trip (every load of a chunk is
+    // issued before the first is waited for; clamped indices re-read in bounds)
+    for (int s0 = 0; s0 < np; s0 += CH) {
+        double mv[CH], pw[CH][IPL];
+        long long rv[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int s = min(s0 + u, np - 1);
+            mv[u] = own ? *gp(A.Mp + mi(A.rows, li, s)) : 0.0;
+            rv[u] = *gp(A.dRp + s);
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) pw[u][k] = *gp(A.Pp + s * A.ld + min(jc0 + tid + k * nth, jc1 - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+            if (s0 + u < np) {
+                if (own) mrowp[s0 + u] = mv[u];
+#pragma unroll
+                for (int k = 0; k < IPL; ++k)
+                    if (jc0 + tid + k * nth < jc1) lPp[(tid + k * nth) * cs + s0 + u] = pw[u][k];
+                if (rv[u] == li) ownpivp |= 1ull << (s0 + u);
+            }
     }
     if (tid < np) sRp[tid] = *gp(A.dRp + tid);
     const long long cap = *gp(&ctl->cap);
@@ -1694,30 +1718,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base)
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
 }
 
-// LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt)
-template <int W, int RW, int NB, int LA = 0, int SA = 0>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(6, 8)))
-k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
-           const double *__restrict__ M, const long long *__restrict__ dR,
-           const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
-           long long run)
+// One strip of 128 columns over rows [r0, r1): the strip's slice of P is
+// staged in LDS (sp), each wave walks RW-row batches and keeps the NEXT
+// batch's rows and multipliers in flight while it applies the pivots to the
+// current one.  Shared by the in-place sweep (one strip and row run per
+// workgroup) and the pipelined sweep (tiles taken from a counter).
+template <int W, int RW, int NB, int LA, int SA>
+__device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)[W][NB][RW / 2],
+                                            const long long (&sr)[NB], const double *T, double *Tout,
+                                            const double *__restrict__ P, const double *__restrict__ M,
+                                            int nd, long long ld, long long rows, int strip,
+                                            long long r0, long long r1)
 {
-    static_assert(RW % 2 == 0 && NB <= BMAX && (NB * RW) % 64 == 0, "k_sweep_st: batch shape");
     constexpr int MPL = NB * RW / 64;           // multipliers per lane per batch
-    __shared__ double2 sp[NB][64];              // the strip's slice of P
-    __shared__ double2 sm[W][NB][RW / 2];       // per wave: the current batch's multipliers
-    __shared__ long long sr[NB];
-    const int nd = (int)ctl->ndef[grp];         // <= NB (the host's bound)
-    if (nd == 0) return;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // block b: strip b % nstrips of row run b / nstrips.  Consecutive blocks
-    // are dealt round-robin over the 8 XCDs, so each run's multipliers and
-    // each strip's slice of P are fetched into every XCD's L2 about once
-    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
-    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
-    const long long r1 = min(rows, r0 + run);
-    if (r0 >= r1) return;
     // lanes past the last column (ld % 128 == 64) shadow the last lane's
     // columns: same loads, same results, same bytes stored
     const long long c0 = (long long)strip * 128;
@@ -1728,7 +1743,6 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
     double *Tos = Tout + c0;
     for (int s = wave; s < NB; s += W)
         sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
-    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
     // element e = lane + 64 q of a batch's multipliers: pivot e / RW, row e % RW
     // (padding pivots read pivot 0's and are zeroed)
     int mof[MPL];
@@ -1813,6 +1827,74 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
 #pragma unroll
         for (int k = 0; k < RW; ++k)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
+    }
+}
+
+// LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt)
+template <int W, int RW, int NB, int LA = 0, int SA = 0>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(6, 8)))
+k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
+           const double *__restrict__ M, const long long *__restrict__ dR,
+           const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
+           long long run)
+{
+    static_assert(RW % 2 == 0 && NB <= BMAX && (NB * RW) % 64 == 0, "k_sweep_st: batch shape");
+    __shared__ double2 sp[NB][64];              // the strip's slice of P
+    __shared__ double2 sm[W][NB][RW / 2];       // per wave: the current batch's multipliers
+    __shared__ long long sr[NB];
+    const int nd = (int)ctl->ndef[grp];         // <= NB (the host's bound)
+    if (nd == 0) return;
+    // block b: strip b % nstrips of row run b / nstrips.  Consecutive blocks
+    // are dealt round-robin over the 8 XCDs, so each run's multipliers and
+    // each strip's slice of P are fetched into every XCD's L2 about once
+    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
+    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
+    const long long r1 = min(rows, r0 + run);
+    if (r0 >= r1) return;
+    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
+    sweep_strip<W, RW, NB, LA, SA>(sp, sm, sr, T, Tout, P, M, nd, ld, rows, strip, r0, r1);
+}
+
+// Pipelined sweep (out of place, beside the next group's one-XCD selection):
+// the workgroups dealt to the selection's XCD (ctl->sel_xcc, published by the
+// selection launch) leave at once, the others take tiles from a counter --
+// nbig tall row runs of run1 rows per strip first, then run2-row runs, so the
+// workgroups finish together whichever of them left.  Which XCD is avoided is
+// a speed matter only: every tile is taken exactly once either way.
+template <int W, int RW, int NB>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(6, 8)))
+k_sweep_tiles(const double *T, double *Tout, const double *__restrict__ P,
+              const double *__restrict__ M, const long long *__restrict__ dR, Ctl *ctl,
+              long long ld, long long rows, int grp, int nstrips, long long run1, long long nbig,
+              long long run2)
+{
+    static_assert(RW % 2 == 0 && NB <= BMAX && (NB * RW) % 64 == 0, "k_sweep_tiles: batch shape");
+    __shared__ double2 sp[NB][64];
+    __shared__ double2 sm[W][NB][RW / 2];
+    __shared__ long long sr[NB];
+    __shared__ long long stile;
+    const int nd = (int)ctl->ndef[grp];
+    if (nd == 0) return;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    if (xcc == ld_sc1(&ctl->sel_xcc)) return;   // uniform over the workgroup
+    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
+    const long long rbig = min(rows, nbig * run1);
+    const long long ntile = (long long)nstrips * (nbig + (rows - rbig + run2 - 1) / run2);
+    for (;;) {
+        __syncthreads();                        // the previous tile's LDS reads are done
+        if (threadIdx.x == 0)
+            stile = (long long)__hip_atomic_fetch_add(gp(&ctl->tiles[grp]), 1ull, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const long long k = stile;
+        if (k >= ntile) break;
+        const int strip = (int)(k % nstrips);
+        const long long q = k / nstrips;
+        const long long r0 = q < nbig ? q * run1 : rbig + (q - nbig) * run2;
+        const long long r1 = min(rows, q < nbig ? r0 + run1 : r0 + run2);
+        if (r0 < r1)
+            sweep_strip<W, RW, NB, 0, 0>(sp, sm, sr, T, Tout, P, M, nd, ld, rows, strip, r0, r1);
     }
 }
 
@@ -2092,9 +2174,26 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
         if (nd_max <= 16) SWEEP_ST_ONE(W, RW, 16, LA, SA);                                   \
         else SWEEP_ST_ONE(W, RW, 32, LA, SA);                                                \
     } while (0)
-    // the pipelined mode's out-of-place sweeps beside a persistent selection
-    // keep k_sweep (a strip sweep there hung a test run; not investigated:
-    // that mode is off by default and measured slower)
+    if (T_out != A.T && variant != 1) {
+        // pipelined: tiles over the CUs of the 7 XCDs the selection leaves
+        // free; tall runs (about 3/4 of the rows, one per workgroup) first,
+        // then 32-row runs to even out the end
+        constexpr int BPC = 3, RUN2 = 32;
+        const long long ns = (A.ld + 127) / 128;
+        const long long slots = (long long)sweep_cus() * 7 / 8 * BPC;
+        const long long nbig = std::max(1LL, slots / ns);
+        long long run1 = (A.rows * 3 / 4) / nbig / RUN2 * RUN2;
+        if (run1 < RUN2) run1 = RUN2;
+        const dim3 grid((unsigned)(sweep_cus() * BPC));
+#define SWEEP_TILES(NBV)                                                                      \
+    hipExtLaunchKernelGGL((k_sweep_tiles<8, 4, NBV>), grid, dim3(64 * 8), 0, s, e0, e1, 0, A.T, T_out, \
+                          A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run1, nbig, (long long)RUN2)
+        if (nd_max <= 16) SWEEP_TILES(16);
+        else SWEEP_TILES(32);
+#undef SWEEP_TILES
+        return hipGetLastError();
+    }
+    // LPGPU_SWEEP=1: the tile sweep k_sweep, also for the pipelined mode
     const int v = T_out != A.T ? 1 : variant;
     switch (v) {
     case 1:
@@ -2115,6 +2214,11 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
     return hipGetLastError();
 }
 
+long long group_blocks_xcd_here(long long rc, long long ld, int count, int lag)
+{
+    return group_blocks_xcd(rc, ld, count, sweep_cus() / 8, lag);
+}
+
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
                         unsigned seq, int bmax, int lag_layout, int xr, const Args *As, int nshard,
                         hipEvent_t e0, hipEvent_t e1)
@@ -2129,7 +2233,7 @@ hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int fr
     long long g = 0;
     // one-XCD selection: single device, or a rank of a sharded job whose
     // ranks all agreed to it (xr == 2: no two ranks share a GPU)
-    const int xmode = (xr != 1 && !As && !lag_layout) ? group_blocks_xcd(rcg, A.ld, bmax, sweep_cus() / 8) : 0;
+    const int xmode = (xr != 1 && !As) ? group_blocks_xcd(rcg, A.ld, bmax, sweep_cus() / 8, lag_layout) : 0;
     if (xmode) g = xmode;
     else g = group_blocks(rcg, A.ld, bmax, lag_layout);
     if (g == 0) return hipErrorInvalidValue;

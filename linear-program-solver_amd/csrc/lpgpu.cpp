@@ -48,11 +48,10 @@ struct lp_handle {
     unsigned long long *gran = nullptr;  // k_group summaries (tagged granules)
     unsigned gseq = 0;              // k_group launches so far (tags their summaries)
     // pipelined groups (single device): group g's sweep (out of place, T -> T2)
-    // runs on its own CUs while group g+1 is selected on the others
-    bool pipeline = false;          // LPGPU_PIPELINE=1: measured slower on cfg3 (memory contention)
+    // runs on seven XCDs while group g+1 is selected on the eighth
+    bool pipeline = false;          // LPGPU_PIPELINE=1
     double *T2 = nullptr;           // second tableau buffer
-    hipStream_t ssel = nullptr, ssw = nullptr;   // CU-partitioned streams
-    int sel_cus = 0;                // CUs of the selection stream
+    hipStream_t ssel = nullptr, ssw = nullptr;   // selection (high priority) / sweep streams
     size_t pev_used = 0;            // events of pev handed out since the last sync
     std::vector<hipEvent_t> pev;    // ordering events, reused per batch
     // row-sharded persistent selection: device-side exchange between ranks
@@ -357,7 +356,6 @@ static int alloc_handle(lp_handle *h)
         h->persistent = std::strcmp(sel, "kernels") != 0;
     if (const char *pl = std::getenv("LPGPU_PIPELINE")) h->pipeline = pl[0] == '1';
     if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
-    if (const char *sc = std::getenv("LPGPU_SEL_CUS")) h->sel_cus = std::atoi(sc);
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
             const size_t sb = (lpk::BMAX * 16 + lpk::GROUP_MAXBLOCKS * lpk::BMAX * 2) * sizeof(long long);
@@ -994,10 +992,10 @@ static int begin_call(const Members &M, const std::vector<Args> &A, int mode, in
 // pipelined groups (single device)
 // ---------------------------------------------------------------------------
 
-// second tableau buffer and two CU-partitioned streams: the latency-bound
-// selection keeps sel_cus CUs to itself, the bandwidth-bound sweep streams on
-// the rest, so neither waits behind the other's waves
-static int ensure_pipeline(lp_handle *h, long long g)
+// second tableau buffer and the two streams of the pipelined mode: the
+// one-XCD selection (high priority: its blocks are dispatched first) and the
+// sweep, whose workgroups keep off the selection's XCD (k_sweep_tiles)
+static int ensure_pipeline(lp_handle *h)
 {
     if (h->T2 && h->ssel && h->ssw) return LP_PIVOTED;
     HCHK(h, hipSetDevice(h->dev));
@@ -1006,24 +1004,10 @@ static int ensure_pipeline(lp_handle *h, long long g)
         HCHK(h, hipMalloc(&h->T2, tbytes));
         HCHK(h, hipMemsetAsync(h->T2, 0, tbytes, h->s));   // padding columns stay 0
     }
-    int ncu = 0;
-    HCHK(h, hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->dev));
-    // one selection block per CU where possible (all G blocks must be
-    // co-resident on the selection CUs)
-    int nsel = h->sel_cus > 0 ? h->sel_cus : (int)std::min<long long>(g, ncu / 2);
-    nsel = std::max(1, std::min(nsel, ncu / 2));
-    // the sweep may be held to fewer CUs (LPGPU_SWEEP_CUS): less bandwidth for
-    // it, less contention for the latency-bound selection beside it
-    int nsw = ncu - nsel;
-    if (const char *sw = std::getenv("LPGPU_SWEEP_CUS")) nsw = std::max(1, std::min(nsw, std::atoi(sw)));
-    std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mw((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) {
-        if (c < nsel) ms[c / 32] |= 1u << (c % 32);
-        else if (c < nsel + nsw) mw[c / 32] |= 1u << (c % 32);
-    }
-    HCHK(h, hipExtStreamCreateWithCUMask(&h->ssel, (uint32_t)ms.size(), ms.data()));
-    HCHK(h, hipExtStreamCreateWithCUMask(&h->ssw, (uint32_t)mw.size(), mw.data()));
-    h->sel_cus = nsel;
+    int lo = 0, hi = 0;
+    HCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HCHK(h, hipStreamCreateWithPriority(&h->ssel, hipStreamNonBlocking, hi));
+    HCHK(h, hipStreamCreateWithPriority(&h->ssw, hipStreamNonBlocking, lo));
     return LP_PIVOTED;
 }
 
@@ -1046,8 +1030,7 @@ static int pev_at(lp_handle *h, size_t k, hipEvent_t *e)
 static int enqueue_pipelined(lp_handle *h, int64_t b, bool &chained, int *ngroups)
 {
     const int B = h->block;
-    const long long g = lpk::group_blocks(h->rc, h->ld, B, 1);
-    CALL(ensure_pipeline(h, g));
+    CALL(ensure_pipeline(h));
     double *buf[2] = {h->T, h->T2};
     size_t ne = 0;
     hipEvent_t e0, esel, last_sel = nullptr;
@@ -1112,8 +1095,13 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         if (limit >= 0) b = std::min(b, limit - done);
         for (lp_handle *x : M) CALL(ensure_log(x, done + b + 1));
         A = args_all(M);
-        const bool pipelined = !h->comm && h->persistent && h->pipeline &&
-                               lpk::group_blocks(h->rc, h->ld, B, 1) > 0;
+        // pipelined only where the lagging selection fits on one XCD (the
+        // sweep then has the other seven to itself) and B <= 16: at cfg3 with
+        // B = 20 and 22 the lagging one-XCD selection timed out in its first
+        // exchange although its blocks should fit two per CU (not understood)
+        const bool pipelined = !h->comm && h->persistent && h->pipeline && B <= 16 &&
+                               lpk::group_blocks(h->rc, h->ld, B, 1) > 0 &&
+                               lpk::group_blocks_xcd_here(h->rc, h->ld, B, 1) > 0;
         int ngroups = 0;
         const int64_t before = done;
         h->pev_used = 0;

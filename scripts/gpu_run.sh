@@ -140,6 +140,26 @@ for step in "$@"; do
             grep -H -o '"value": [0-9.]*\|"us_per_pivot": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_dist2*.log ;;
         stamps)
             run stamps 300 python scripts/diag_stamps.py ;;
+        xpipe)
+            # selection on one XCD beside the sweep on the other seven
+            LPGPU_PIPELINE=1 run pytest_xpipe 600 python -u -m pytest tests/test_gpu_parity.py -q -x -p no:cacheprovider --timeout 60 --timeout-method thread
+            run bench_xp_np 300 python bench.py --no-cpu-baseline --steps 1024
+            for B in ${XP_BLOCKS:-8 12 16 20 22}; do
+                LPGPU_PIPELINE=1 run bench_xp_b$B 300 python bench.py --no-cpu-baseline --steps 1024 --block $B
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_xp_*.log ;;
+        xpdiag)
+            LPGPU_DEBUG_XCC=1 run bench_xd_np 300 python bench.py --no-cpu-baseline --steps 1024 --block 16
+            LPGPU_DEBUG_XCC=1 LPGPU_PIPELINE=1 run bench_xd_p16 300 python bench.py --no-cpu-baseline --steps 1024 --block 16
+            LPGPU_DEBUG_XCC=1 LPGPU_PIPELINE=1 LPGPU_PIPE_SERIAL=1 run bench_xd_s16 300 python bench.py --no-cpu-baseline --steps 1024 --block 16
+            for f in "$OUT"/bench_xd_*.log; do echo $f; grep -o 'sel_xcc [0-9]*' $f | sort | uniq -c; done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_xd_*.log ;;
+        tall1)
+            # the whole weak-scaling tableau of N ranks on ONE GPU (rows 4096 N)
+            for E in ${TALL_RANKS:-2 4 8}; do
+                run bench_tall1_e$E 600 python bench.py --no-cpu-baseline --emulate-ranks $E --steps 256
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_tall1_e*.log ;;
         pmc)
             export TMPDIR=/tmp
             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline

@@ -376,3 +376,18 @@ def test_sharded_one_exchange_band_and_straddle(kind, tie, nshards, k, shard_mod
         assert olog.tolist() == [[1, 0]]
     for g in reversed(grp):
         g.close()
+
+
+@pytest.mark.parametrize("ns", [12200, 13300])
+def test_one_xcd_selection_at_lds_edge(ns):
+    """wide tableaux whose persistent selection blocks need 66-73 KB of LDS
+    each (two per CU on one XCD, the edge of group_blocks_xcd's sizing):
+    the launch must not stall and the rows stay bit-identical to the oracle"""
+    T = gen.tableau("tall", 4096, ns, 17)
+    e = engine_of(T, 32)
+    st, done = e.run(_lib.RULE_STANDARD, 40)
+    o = F64Tableau(T)
+    ost, olog = o.run(0, 40)
+    assert e.log().tolist() == olog.tolist()
+    assert np.array_equal(e.download(), o.T)
+    e.close()
