@@ -236,7 +236,10 @@ inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus
     if (g4 > g) g = g4;
     if (g < 1) g = 1;
     if (g > GROUP_MAXBLOCKS) return 0;
-    const long long per_cu = 160 * 1024 / (group_lds(rc, ld, g, count, lag) + 4096);   // + static LDS
+    // blocks per CU: LDS-bound, and at most one single-wave block per SIMD
+    // (k_group takes up to 256 VGPRs: one wave per SIMD is all that is sure)
+    long long per_cu = 160 * 1024 / (group_lds(rc, ld, g, count, lag) + 4096);   // + static LDS
+    if (per_cu > 4) per_cu = 4;
     return per_cu >= 1 && g <= per_cu * cus ? g : 0;
 }
 // group_blocks_xcd for this device (0: the shape does not fit one XCD)

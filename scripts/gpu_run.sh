@@ -154,6 +154,12 @@ for step in "$@"; do
             LPGPU_DEBUG_XCC=1 LPGPU_PIPELINE=1 LPGPU_PIPE_SERIAL=1 run bench_xd_s16 300 python bench.py --no-cpu-baseline --steps 1024 --block 16
             for f in "$OUT"/bench_xd_*.log; do echo $f; grep -o 'sel_xcc [0-9]*' $f | sort | uniq -c; done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_xd_*.log ;;
+        big1)
+            run pytest_big 600 python -u -m pytest tests/test_gpu_parity.py -k "block_count or lds_edge or cfg3_full" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for E in 4 8; do
+                run bench_big_e$E 600 python bench.py --no-cpu-baseline --emulate-ranks $E --steps 256
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_big_e*.log ;;
         tall1)
             # the whole weak-scaling tableau of N ranks on ONE GPU (rows 4096 N)
             for E in ${TALL_RANKS:-2 4 8}; do

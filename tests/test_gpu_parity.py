@@ -391,3 +391,19 @@ def test_one_xcd_selection_at_lds_edge(ns):
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), o.T)
     e.close()
+
+
+@pytest.mark.parametrize("m,ns,block", [(10000, 300, 32), (16000, 600, 7), (8192, 2000, 16)])
+def test_one_xcd_selection_block_count(m, ns, block, select_mode):
+    """tall, narrow tableaux: 125-250 selection blocks whose LDS would let
+    far more than four share a CU; one XCD holds them only if at most one
+    single-wave block per SIMD is assumed (otherwise the launch stalls and
+    times out) -- same pivots and bit-identical rows as the oracle"""
+    T = gen.tableau("tall", m, ns, 23)
+    e = engine_of(T, block)
+    st, done = e.run(_lib.RULE_STANDARD, 48)
+    o = F64Tableau(T)
+    ost, olog = o.run(0, 48)
+    assert e.log().tolist() == olog.tolist()
+    assert np.array_equal(e.download(), o.T)
+    e.close()
