@@ -160,6 +160,14 @@ for step in "$@"; do
                 run bench_big_e$E 600 python bench.py --no-cpu-baseline --emulate-ranks $E --steps 256
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_big_e*.log ;;
+        tiles)
+            LPGPU_SWEEP=41 run pytest_tiles 300 python -u -m pytest tests/test_gpu_parity.py -k "cfg3_full and persistent" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2; do
+                for V in 21 40 41; do
+                    LPGPU_SWEEP=$V run bench_tl${V}_$rep 300 python bench.py --no-cpu-baseline --steps 1024
+                done
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_tl*.log ;;
         tall1)
             # the whole weak-scaling tableau of N ranks on ONE GPU (rows 4096 N)
             for E in ${TALL_RANKS:-2 4 8}; do
