@@ -865,7 +865,10 @@ __device__ long long combine_loaded(const double (&l)[NR], const long long (&i)[
     return NONE;
 }
 
-constexpr int CH = 8;    // deferred pivots applied per chunk (loads issued together)
+#ifndef LPK_CH
+#define LPK_CH 8
+#endif
+constexpr int CH = LPK_CH;    // deferred pivots applied per chunk (loads issued together)
 
 // ---- row-sharded persistent selection (XR): device-side exchange between
 // ranks through each rank's exchange buffer (xbuf), written by its peers over
