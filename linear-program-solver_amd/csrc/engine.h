@@ -34,7 +34,7 @@ constexpr int PICK_CHECK = 1;     // owner validates the requested row (Simplex.
 constexpr int PICK_EXPLICIT = 2;  // owner contributes the requested row (Tableau.pivot)
 constexpr int PICK_LOCAL = 3;     // first local row within the LOCAL band + (l, q)
 
-constexpr int BMAX = 32;           // most pivots deferred into one sweep
+constexpr int BMAX = 64;           // most pivots deferred into one sweep
 constexpr int RATIO_THREADS = 256;
 constexpr int RATIO_CHUNK = 256;   // rows per ratio block (one per thread)
 constexpr int PROW_THREADS = 256;  // columns per pivot-row block (one per thread)

@@ -763,7 +763,7 @@ __device__ __forceinline__ long long un_idx(unsigned w) { return w == 0x7fffffff
 // 7 is the setup ping (never a pivot's tag)
 __device__ __forceinline__ unsigned gtag(unsigned seq, int t, int ph)
 {
-    return seq * (8 * BMAX) + 8 * t + ph;     // seq < 2^24 (the host wraps it)
+    return seq * (8 * BMAX) + 8 * t + ph;     // seq < 2^23 (the host wraps it)
 }
 
 // hand-off store of k_group.  fast: every block of the launch runs on ONE XCD
@@ -1835,7 +1835,7 @@ __device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)
 
 // LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt)
 template <int W, int RW, int NB, int LA = 0, int SA = 0>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(6, 8)))
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(NB <= 32 ? 6 : 2, 8)))
 k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
            const double *__restrict__ M, const long long *__restrict__ dR,
            const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
@@ -2066,7 +2066,7 @@ __global__ void k_group_min(double *const *ptrs, int n)
 // compile-time bound of the deferred-pivot count: 0, 1, 2, 4, 8, 16, 32
 static int bound_of(int t)
 {
-    return t <= 0 ? 0 : t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : t <= 8 ? 8 : t <= 16 ? 16 : 32;
+    return t <= 0 ? 0 : t <= 1 ? 1 : t <= 2 ? 2 : t <= 4 ? 4 : t <= 8 ? 8 : t <= 16 ? 16 : t <= 32 ? 32 : 64;
 }
 
 #define TP_DISPATCH(t, KERNEL, ...)                                                           \
@@ -2077,7 +2077,8 @@ static int bound_of(int t)
     case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                                 \
     case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                                 \
     case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                               \
-    default: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                               \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                               \
+    default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                               \
     }
 
 hipError_t launch_reset(hipStream_t s, const Args &A, int mode, int rule, int chain, long long cap,
@@ -2168,14 +2169,18 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
 #define SWEEP_ST_LAUNCH(W, RW, BPC, LA, SA)                                                  \
     do {                                                                                     \
         const long long ns = (A.ld + 127) / 128;                                             \
-        long long nrun = (long long)sweep_cus() * (BPC) / ns;                                \
+        /* 48 / 64 pivots: the strip's slice of P takes 48 / 64 KB of LDS */               \
+        const int bpc_ = nd_max <= 32 ? (BPC) : nd_max <= 48 ? 2 : 1;                       \
+        long long nrun = (long long)sweep_cus() * bpc_ / ns;                                 \
         if (nrun < 1) nrun = 1;                                                              \
         long long run = (A.rows + nrun - 1) / nrun;                                          \
         run = (run + (RW) - 1) / (RW) * (RW);                                                \
         nrun = (A.rows + run - 1) / run;                                                     \
         const dim3 grid((unsigned)(nrun * ns));                                              \
         if (nd_max <= 16) SWEEP_ST_ONE(W, RW, 16, LA, SA);                                   \
-        else SWEEP_ST_ONE(W, RW, 32, LA, SA);                                                \
+        else if (nd_max <= 32) SWEEP_ST_ONE(W, RW, 32, LA, SA);                              \
+        else if (nd_max <= 48) SWEEP_ST_ONE(W, RW, 48, LA, SA);                              \
+        else SWEEP_ST_ONE(W, RW, 64, LA, SA);                                                \
     } while (0)
     if (T_out != A.T && variant != 1) {
         // pipelined: tiles over the CUs of the 7 XCDs the selection leaves

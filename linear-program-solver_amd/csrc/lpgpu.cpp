@@ -767,7 +767,7 @@ extern "C" int lp_upload_rows(lp_handle *h, int64_t row0, int64_t nrows, const d
 extern "C" int lp_set_block(lp_handle *h, int pivots_per_sweep)
 {
     if (pivots_per_sweep < 1 || pivots_per_sweep > lpk::BMAX)
-        return fail(h, LP_BAD_ARG, "pivots_per_sweep must be in [1, 32]");
+        return fail(h, LP_BAD_ARG, "pivots_per_sweep must be in [1, 64]");
     for (lp_handle *x : members_of(h))
         if (x) x->block = pivots_per_sweep;
     return LP_PIVOTED;
@@ -843,7 +843,7 @@ static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int g
                               const Args *As = nullptr, int nshard = 1)
 {
     // every rank of a sharded job advances gseq identically (same calls, same order)
-    h->gseq = h->gseq % ((1u << 24) - 1) + 1;
+    h->gseq = h->gseq % ((1u << 23) - 1) + 1;   // gtag: seq * 8 * BMAX fits 32 bits
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 1));
     HCHK(h, lpk::launch_group(st, A, grp, cnt, from_erec, h->gseq, h->block, lag_layout, xr, As,
@@ -1091,8 +1091,10 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
     int grp = 0;
     bool chained = false;  // the next pivot's entering column comes from k_prow
     for (;;) {
+        // a known pivot count goes in one batch (launches after a stop exit
+        // at once); open-ended solves grow their batches
         int64_t b = batch;
-        if (limit >= 0) b = std::min(b, limit - done);
+        if (limit >= 0) b = std::min<int64_t>(limit - done, std::max<int64_t>(batch, 1 << 15));
         for (lp_handle *x : M) CALL(ensure_log(x, done + b + 1));
         A = args_all(M);
         // pipelined only where the lagging selection fits on one XCD (the

@@ -294,7 +294,7 @@ class Engine:
         return out
 
     def set_block(self, pivots_per_sweep: int):
-        """pivots deferred into one sweep of the tableau (1..32)"""
+        """pivots deferred into one sweep of the tableau (1..64)"""
         self._check(self.lib.lp_set_block(self.h, int(pivots_per_sweep)), self.h)
 
     def get_block(self) -> int:

@@ -14,7 +14,8 @@ e.upload(T)
 e.set_block(16)
 e.run(0, 64)
 e.run(0, 16)
-buf = (C.c_longlong * (32 * 16))()
+BMAX = 64                      # lpk::BMAX: stamp rows per group
+buf = (C.c_longlong * (BMAX * 16))()
 assert e.lib.lpdiag_stamps(e.h, buf) == 0
 # stamp k marks the END of segment names[k-1]; segment 13 runs to the next pivot's stamp 0
 names = ["enter", "col0", "rload", "rcomp", "rpub", "gathR", "leave",
@@ -34,13 +35,13 @@ print("pcomp split: chain=%.2f div=%.2f store=%.2f" % tuple(sum(x[i] for x in su
 
 # per-block publish times: spread across blocks and the last blocks
 G = 65
-bb = (C.c_longlong * (256 * 32 * 2))()
+bb = (C.c_longlong * (256 * BMAX * 2))()
 assert e.lib.lpdiag_bstamps(e.h, bb) == 0
 spread = [[], []]
 last = {}
 for t in range(1, 15):
     for k in (0, 1):
-        v = [bb[(b * 32 + t) * 2 + k] for b in range(G)]
+        v = [bb[(b * BMAX + t) * 2 + k] for b in range(G)]
         v = [x for x in v if x]
         if not v:
             continue

@@ -168,6 +168,15 @@ for step in "$@"; do
                 done
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_tl*.log ;;
+        bsz)
+            # pivots per sweep beyond 32 (BMAX 64)
+            run pytest_bsz 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2; do
+                for B in ${BSZ:-32 40 44 48}; do
+                    run bench_bsz${B}_$rep 300 python bench.py --no-cpu-baseline --steps 1056 --block $B
+                done
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_bsz*.log ;;
         tall1)
             # the whole weak-scaling tableau of N ranks on ONE GPU (rows 4096 N)
             for E in ${TALL_RANKS:-2 4 8}; do

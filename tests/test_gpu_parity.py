@@ -201,7 +201,7 @@ def test_optimal_at_start_and_cap():
     # past the persistent kernel's limits: > 256 blocks x 64 rows, > 256 x 256 columns
     ("tall", 16500, 3, 12), ("tall", 2, 66000, 6),
 ])
-@pytest.mark.parametrize("block", [1, 7, 32])
+@pytest.mark.parametrize("block", [1, 7, 32, 48])
 def test_ragged_shapes_bit_exact(kind, m, ns, k, block, select_mode):
     T = gen.tableau(kind, m, ns, 77)
     e = engine_of(T, block)
@@ -212,7 +212,7 @@ def test_ragged_shapes_bit_exact(kind, m, ns, k, block, select_mode):
     assert np.array_equal(e.download(), o.T)
 
 
-@pytest.mark.parametrize("block", [1, 32])
+@pytest.mark.parametrize("block", [1, 32, 44, 64])
 def test_cfg3_full_size_bit_exact(block, select_mode):
     """4096 x 8192 (the 1-GPU roofline config): 40 standard pivots, whole
     268 MB tableau bit-identical to the f64 oracle."""
@@ -241,7 +241,7 @@ def shard_mode(request, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("block", [1, 6, 32])
+@pytest.mark.parametrize("block", [1, 6, 32, 48])
 @pytest.mark.parametrize("nshards", [1, 2, 3, 5, 8])
 def test_sharded_group_invariance(nshards, block, shard_mode):
     """Row-sharded protocol (allreduce-min + slot allgather) emulated in one
@@ -317,7 +317,7 @@ def test_block_size_invariance(select_mode):
     per-pivot float64 operations)"""
     T = gen.tableau("mixed", 200, 300, 5)
     outs = []
-    for block in (1, 2, 3, 8, 13, 31, 32):
+    for block in (1, 2, 3, 8, 13, 31, 32, 33, 44, 48, 57, 64):
         e = engine_of(T, block)
         e.run(_lib.RULE_STANDARD, 70)
         outs.append((e.log().tolist(), e.download()))
