@@ -177,6 +177,14 @@ for step in "$@"; do
                 done
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_bsz*.log ;;
+        msw)
+            LPGPU_SWEEP=50 run pytest_msw 600 python -u -m pytest tests/test_gpu_parity.py -k "cfg3_full or ragged or block_size" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2; do
+                for V in 21 50; do
+                    LPGPU_SWEEP=$V run bench_msw${V}_$rep 300 python bench.py --no-cpu-baseline --steps 1024
+                done
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_msw*.log ;;
         tall1)
             # the whole weak-scaling tableau of N ranks on ONE GPU (rows 4096 N)
             for E in ${TALL_RANKS:-2 4 8}; do
