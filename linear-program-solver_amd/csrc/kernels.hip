@@ -1554,22 +1554,24 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 7) wv = hi32(p0n);
             publish(&grE[b * 8], gtag(seq, t, 1), wv, NGE, fast);
         }
-        // records read after the launch only (host, sweep, next launch)
-        if (b == 0 && tid == 0) {
-            st_x(&A.dR[t], R, fast);
-            st_x(&A.dC[t], C, fast);
-            st_x(&ctl->r, rglob, fast);
-            if (npiv < A.logcap) {
-                *gp(A.log + 2 * npiv) = rglob;
-                *gp(A.log + 2 * npiv + 1) = C - 1;
-            }
-            st_x(&ctl->npiv, npiv + 1, fast);
-            st_x(&ctl->ndef[grp], (long long)(t + 1), fast);
-            if (mode == MODE_SOLVE) {
-                st_x(&ctl->nstd, nstd, fast);
-                st_x(&ctl->stuck, stuck, fast);
-                st_x(&ctl->rule, (int)rule, fast);
-            }
+        // records read after the launch only (host, sweep, next launch): one
+        // store instruction of the last block (block 0 already carries the
+        // stall bookkeeping and column 0), one record per lane
+        if (b == G - 1 && tid < 7) {
+            long long *adr = &A.dR[t];
+            long long val = R;
+            if (tid == 1) { adr = &A.dC[t]; val = C; }
+            else if (tid == 2) { adr = &ctl->r; val = rglob; }
+            else if (tid == 3) { adr = &ctl->npiv; val = npiv + 1; }
+            else if (tid == 4) { adr = &ctl->ndef[grp]; val = t + 1; }
+            else if (tid == 5) { adr = A.log + 2 * min(npiv, A.logcap - 1); val = rglob; }
+            else if (tid == 6) { adr = A.log + 2 * min(npiv, A.logcap - 1) + 1; val = C - 1; }
+            if (tid < 5 || npiv < A.logcap) st_x(adr, val, fast);
+        }
+        if (b == 0 && tid == 0 && mode == MODE_SOLVE) {
+            st_x(&ctl->nstd, nstd, fast);
+            st_x(&ctl->stuck, stuck, fast);
+            st_x(&ctl->rule, (int)rule, fast);
         }
         if (t == count - 1 && tid == 0) {     // the next launch reads plain summaries
             st_x(&A.erec[b].l, el, fast);
