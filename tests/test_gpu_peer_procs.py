@@ -1,4 +1,4 @@
-"""Row-sharded job as two PROCESSES on one GPU with the device-side peer
+"""Row-sharded job as 2, 4 or 8 PROCESSES on one GPU with the device-side peer
 exchange (IPC handles, peer stores, ping check): the multi-process plumbing
 of the 8-GPU job, bit-identical to the f64 oracle."""
 import os
@@ -18,20 +18,25 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,m,ns,k,block,tie,mode", [
-    ("mixed", 200, 150, 60, 8, 1e-12, "peer"),
-    ("tall", 300, 40, 50, 32, 1e-12, "peer"),
-    ("mixed", 48, 32, 40, 4, 0.25, "peer"),       # wide tie band: straddles across ranks
-    ("mixed", 120, 90, 20, 8, 1e-12, "scan"),     # + column scans, explicit pivots (host all-gather)
-    ("pos", 64, 64, 10, 4, 1e-12, "scan"),
-    ("mixed", 60, 50, 30, 8, 1e-12, "host"),      # every exchange through the host all-gather
+@pytest.mark.parametrize("kind,m,ns,k,block,tie,mode,world", [
+    ("mixed", 200, 150, 60, 8, 1e-12, "peer", 2),
+    ("tall", 300, 40, 50, 32, 1e-12, "peer", 2),
+    ("mixed", 48, 32, 40, 4, 0.25, "peer", 2),       # wide tie band: straddles across ranks
+    ("mixed", 120, 90, 20, 8, 1e-12, "scan", 2),     # + column scans, explicit pivots (host all-gather)
+    ("pos", 64, 64, 10, 4, 1e-12, "scan", 2),
+    ("mixed", 60, 50, 30, 8, 1e-12, "host", 2),      # every exchange through the host all-gather
+    # the rank counts of the driver's scaling runs (processes sharing the one GPU)
+    ("mixed", 200, 150, 60, 8, 1e-12, "peer", 4),
+    ("mixed", 48, 32, 40, 4, 0.25, "peer", 4),
+    ("tall", 400, 40, 50, 32, 1e-12, "peer", 8),
+    ("mixed", 120, 90, 20, 8, 1e-12, "scan", 4),
 ])
-def test_two_process_peer_exchange(kind, m, ns, k, block, tie, mode):
+def test_multi_process_peer_exchange(kind, m, ns, k, block, tie, mode, world):
     port = _free_port()
     procs = []
-    for rank in range(2):
+    for rank in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                   WORLD_SIZE="2", LOCAL_RANK="0")
+                   WORLD_SIZE=str(world), LOCAL_RANK="0")
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(HERE, "_peer_worker.py"), kind, str(m), str(ns), str(k),
              str(block), str(tie), mode], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
