@@ -334,17 +334,7 @@ class Engine:
         see gloo_allgather).  The column scans combine through it; a handle
         without an RCCL communicator also runs its per-pivot exchanges
         through it."""
-        def tramp(ctx, send, recv, nbytes):
-            try:
-                parts = fn(C.string_at(send, nbytes))
-                blob = b"".join(parts)
-                if len(blob) != nbytes * len(parts):
-                    return 1
-                C.memmove(recv, blob, len(blob))
-                return 0
-            except Exception:       # noqa: BLE001 - no exception may cross the C ABI
-                return 1
-        cb = _ALLGATHER_FN(tramp)
+        cb = allgather_callback(fn)
         self._check(self.lib.lp_set_host_allgather(self.h, C.cast(cb, C.c_void_p), None), self.h)
         self._allgather_cb = cb     # the library holds the pointer: keep it alive
 
@@ -356,6 +346,21 @@ class Engine:
 
 
 _ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+
+
+def allgather_callback(fn):
+    """The C callback (lp_allgather_fn) around fn(bytes) -> [bytes per rank]."""
+    def tramp(ctx, send, recv, nbytes):
+        try:
+            parts = fn(C.string_at(send, nbytes))
+            blob = b"".join(parts)
+            if len(blob) != nbytes * len(parts):
+                return 1
+            C.memmove(recv, blob, len(blob))
+            return 0
+        except Exception:       # noqa: BLE001 - no exception may cross the C ABI
+            return 1
+    return _ALLGATHER_FN(tramp)
 
 
 def gloo_allgather(group=None):

@@ -93,3 +93,39 @@ def test_sharded_protocol_matches_unsharded(tmp_path, world, kind, m, ns, k, tol
         assert log.tolist() == [[1, 0]]
         if world == 2:
             assert sum(int(r["slow"]) for r in res) == world, "rare branch not exercised"
+
+
+def _cb_worker(rank, world, port, out):
+    import ctypes as C
+    import sys
+    for p in (PKG, ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from lpsol_amd import _lib
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    cb = _lib.allgather_callback(_lib.gloo_allgather())
+    send = bytes((rank * 17 + i) % 256 for i in range(40))      # one rank's 40-byte record
+    sbuf = C.create_string_buffer(send, len(send))
+    rbuf = C.create_string_buffer(len(send) * world)
+    rc = cb(None, C.cast(sbuf, C.c_void_p), C.cast(rbuf, C.c_void_p), len(send))
+    # a failing host collective reports 1 instead of raising through the C ABI
+    bad = _lib.allgather_callback(lambda data: [data[:-1]])(None, C.cast(sbuf, C.c_void_p),
+                                                           C.cast(rbuf, C.c_void_p), len(send))
+    np.save(os.path.join(out, f"cb{rank}.npy"), np.frombuffer(rbuf.raw, dtype=np.uint8))
+    with open(os.path.join(out, f"rc{rank}"), "w") as f:
+        f.write(f"{rc} {bad}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_allgather_callback(tmp_path, world):
+    """the lp_allgather_fn the engine calls for multi-process column scans
+    (lp_set_host_allgather) over gloo: every rank's bytes, in rank order"""
+    port = _free_port()
+    mp.spawn(_cb_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    want = np.concatenate([np.array([(r * 17 + i) % 256 for i in range(40)], dtype=np.uint8)
+                           for r in range(world)])
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"cb{r}.npy"), want)
+        assert open(tmp_path / f"rc{r}").read() == "0 1"
