@@ -78,6 +78,37 @@ __global__ void __launch_bounds__(512) k_strip(double *T, long long ld, long lon
     }
 }
 
+// the same, runs interleaved: workgroup j of a strip takes the 32-row batches
+// j, j + nrun, j + 2 nrun, ... so every workgroup works inside one moving
+// window of nrun x 32 rows
+template <int NF>
+__global__ void __launch_bounds__(512) k_strip_il(double *T, long long ld, long long rows, int nstrips,
+                                                  int nrun, double s)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int strip = blockIdx.x % nstrips;
+    const int j = blockIdx.x / nstrips;
+    const long long c = (long long)strip * 128 + lane * 2;
+    if (c + 1 >= ld) return;
+    for (long long bb = j; bb * 32 < rows; bb += nrun) {
+        const long long rb = bb * 32 + wave * 4;
+        if (rb >= rows) continue;
+        double2 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = *reinterpret_cast<double2 *>(T + min(rb + k, rows - 1) * ld + c);
+#pragma unroll
+        for (int f = 0; f < (NF > 0 ? NF : 1); ++f)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x[k].x = NF > 0 ? fma(-s, 1e-300, x[k].x) : x[k].x * s;
+                x[k].y = NF > 0 ? fma(-s, 1e-300, x[k].y) : x[k].y * s;
+            }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (rb + k < rows) *reinterpret_cast<double2 *>(T + (rb + k) * ld + c) = x[k];
+    }
+}
+
 int main()
 {
     const long long n = 4097LL * 8256LL;     // cfg3: (m + 1) x ld doubles
@@ -144,6 +175,29 @@ int main()
                 std::printf("{\"pattern\": \"strip-inplace\", \"fma_per_element\": %d, \"workgroups_per_cu\": %d, \"us\": %.1f, \"GBps\": %.0f}\n",
                             nf, bpc, med * 1e6, bytes / med / 1e9);
             }
+        }
+    }
+    // strip pattern, runs interleaved into one moving window
+    {
+        const long long ld = 8256, rows = 4097;
+        const int ns = (int)((ld + 127) / 128);
+        const int nrun = ncu * 3 / ns;
+        for (int nf : {0, 32}) {
+            std::vector<float> ms;
+            for (int it = 0; it < 23; ++it) {
+                CK(hipEventRecord(e0, 0));
+                if (nf == 0) hipLaunchKernelGGL(k_strip_il<0>, dim3(nrun * ns), dim3(512), 0, 0, (double *)a, ld, rows, ns, nrun, 1.0);
+                else hipLaunchKernelGGL(k_strip_il<32>, dim3(nrun * ns), dim3(512), 0, 0, (double *)a, ld, rows, ns, nrun, 1.0);
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float t = 0.f;
+                CK(hipEventElapsedTime(&t, e0, e1));
+                if (it >= 3) ms.push_back(t);
+            }
+            std::sort(ms.begin(), ms.end());
+            const double med = ms[ms.size() / 2] * 1e-3;
+            std::printf("{\"pattern\": \"strip-inplace-interleaved\", \"fma_per_element\": %d, \"us\": %.1f, \"GBps\": %.0f}\n",
+                        nf, med * 1e6, 2.0 * n * 8 / med / 1e9);
         }
     }
     // the same in-place pass over a 2x larger buffer (does not fit the 256 MB Infinity Cache)
