@@ -244,6 +244,8 @@ inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus
 }
 // group_blocks_xcd for this device (0: the shape does not fit one XCD)
 long long group_blocks_xcd_here(long long rc, long long ld, int count, int lag);
+// can the pipelined mode's lagging selection share the device with the sweep?
+int pipeline_fits(long long rc, long long ld, int count);
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
 
 // per-column statistics of the local constraint rows (row 0 excluded)

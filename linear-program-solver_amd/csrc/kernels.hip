@@ -2229,6 +2229,18 @@ long long group_blocks_xcd_here(long long rc, long long ld, int count, int lag)
     return group_blocks_xcd(rc, ld, count, sweep_cus() / 8, lag);
 }
 
+// the pipelined mode's lagging one-XCD selection beside the sweep: at most two
+// blocks per CU, leaving LDS for a 16-pivot sweep workgroup next to them (a
+// full XCD -- four blocks per CU, or two of 66 KB or more -- stalled past the
+// exchange timeout in tests while the sweep ran beside it)
+int pipeline_fits(long long rc, long long ld, int count)
+{
+    const long long g = group_blocks_xcd(rc, ld, count, sweep_cus() / 8, 1);
+    if (g == 0 || g > 2LL * (sweep_cus() / 8)) return 0;
+    const long long lds = group_lds(rc, ld, g, count, 1) + 4096;
+    return 2 * lds + 20 * 1024 <= 160 * 1024 ? 1 : 0;
+}
+
 hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
                         unsigned seq, int bmax, int lag_layout, int xr, const Args *As, int nshard,
                         hipEvent_t e0, hipEvent_t e1)

@@ -1097,13 +1097,11 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         if (limit >= 0) b = std::min<int64_t>(limit - done, std::max<int64_t>(batch, 1 << 15));
         for (lp_handle *x : M) CALL(ensure_log(x, done + b + 1));
         A = args_all(M);
-        // pipelined only where the lagging selection fits on one XCD (the
-        // sweep then has the other seven to itself) and B <= 16: at cfg3 with
-        // B = 20 and 22 the lagging one-XCD selection timed out in its first
-        // exchange although its blocks should fit two per CU (not understood)
+        // pipelined only where the lagging selection fits on one XCD with
+        // room to spare (the sweep has the other seven) and B <= 16
         const bool pipelined = !h->comm && h->persistent && h->pipeline && B <= 16 &&
                                lpk::group_blocks(h->rc, h->ld, B, 1) > 0 &&
-                               lpk::group_blocks_xcd_here(h->rc, h->ld, B, 1) > 0;
+                               lpk::pipeline_fits(h->rc, h->ld, B) != 0;
         int ngroups = 0;
         const int64_t before = done;
         h->pev_used = 0;
