@@ -113,6 +113,65 @@ def cpu_baseline(seconds_target: float = 15.0) -> dict:
             "seconds_per_pivot": sec_per_pivot}
 
 
+def config_table(cpu_budget: float = 20.0) -> None:
+    """--configs: BASELINE.json's small configs on GPU 0, each next to the
+    reference's algorithm on one host core (the exact-Fraction restatement,
+    oracle/exact.py: the cpu_baseline leg), one JSON line per config.  GPU
+    legs are whole calls (upload excluded), best of 3; CPU legs run to the end
+    or for cpu_budget seconds (then per pivot)."""
+    from oracle import exact
+
+    def gpu(T, job):
+        best, n = None, 0
+        for _ in range(3):
+            e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+            e.upload(T)
+            t0 = time.perf_counter()
+            if job == "solve":
+                e.solve()
+            else:
+                e.run(_lib.RULE_STANDARD, job)
+            dt = time.perf_counter() - t0
+            n = len(e.log())
+            e.close()
+            best = dt if best is None else min(best, dt)
+        return best, n
+
+    def cpu(T, job):
+        F = exact.from_array(T)
+        t0 = time.perf_counter()
+        if job == "solve" and T.size <= 20000:
+            res = exact.solve(F)
+            return time.perf_counter() - t0, len(res["seq"]), True
+        done, k = 0, (1 << 30 if job == "solve" else job)
+        while done < k and time.perf_counter() - t0 < cpu_budget:
+            p = exact.find_standard(F)
+            if isinstance(p, str):
+                break
+            exact.pivot(F, *p)
+            done += 1
+        return time.perf_counter() - t0, done, False
+
+    cases = [
+        ("cfg1", "G_pos 8 x 10 + 8 slacks, Simplex.solve", gen.tableau("pos", 8, 10, 1), "solve"),
+        ("cfg2", "G_pos 512 x 512 + 512 slacks (512 x 1024), Simplex.solve",
+         gen.tableau("pos", 512, 512, 2), "solve"),
+        ("cfg2", "G_mixed 512 x 512 + 512 slacks (512 x 1024), 256 standard pivots",
+         gen.tableau("mixed", 512, 512, 2), 256),
+        ("cfg5", "degenerate Klee-Minty d = 10, Simplex.solve", gen.klee_minty(10, True), "solve"),
+    ]
+    for cfg, what, T, job in cases:
+        tg, ng = gpu(T, job)
+        tc, nc, whole = cpu(T, job)
+        print(json.dumps({
+            "config": cfg, "workload": what, "gpu_s": tg, "gpu_pivots": ng,
+            "gpu_pivots_per_s": ng / tg,
+            "cpu_s": tc, "cpu_pivots": nc, "cpu_whole_run": whole,
+            "cpu_pivots_per_s": nc / tc if tc > 0 else None,
+            "cpu_kind": "port: oracle/exact.py (Fraction), 1 core",
+        }), flush=True)
+
+
 def load_traffic(path: str | None, block: int):
     """HBM bytes per sweep launch measured by scripts/hbm_traffic.py (two
     rocprofv3 --pmc passes on this workload), or None if not measured for
@@ -147,7 +206,13 @@ def main():
     ap.add_argument("--group-shards", type=int, default=0,
                     help="1-GPU diagnostic: the N-rank row-sharded job as N in-process shards "
                          "on one GPU (device copies instead of RCCL)")
+    ap.add_argument("--configs", action="store_true",
+                    help="instead of the benchmark: cfg1/cfg2/cfg5 on GPU 0 next to the "
+                         "exact-Fraction CPU path, one JSON line each")
     args = ap.parse_args()
+    if args.configs:
+        config_table()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
