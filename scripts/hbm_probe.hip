@@ -109,6 +109,42 @@ __global__ void __launch_bounds__(512) k_strip_il(double *T, long long ld, long 
     }
 }
 
+// strips of 256 columns: each lane 32 contiguous bytes per row (two 16-byte
+// accesses), so one wave-instruction pair covers 2 KB of a row
+template <int NF>
+__global__ void __launch_bounds__(512) k_strip256(double *T, long long ld, long long rows, int nstrips,
+                                                  long long run, double s)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int strip = blockIdx.x % nstrips;
+    const long long r0 = (long long)(blockIdx.x / nstrips) * run, r1 = min(rows, r0 + run);
+    const long long c = (long long)strip * 256 + lane * 4;
+    if (c + 3 >= ld) return;
+    for (long long rb = r0 + wave * 4; rb < r1; rb += 32) {
+        double2 x[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                x[k][h] = *reinterpret_cast<double2 *>(T + min(rb + k, r1 - 1) * ld + c + 2 * h);
+#pragma unroll
+        for (int f = 0; f < (NF > 0 ? NF : 1); ++f)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    x[k][h].x = NF > 0 ? fma(-s, 1e-300, x[k][h].x) : x[k][h].x * s;
+                    x[k][h].y = NF > 0 ? fma(-s, 1e-300, x[k][h].y) : x[k][h].y * s;
+                }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (rb + k < r1)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    *reinterpret_cast<double2 *>(T + (rb + k) * ld + c + 2 * h) = x[k][h];
+    }
+}
+
 int main()
 {
     const long long n = 4097LL * 8256LL;     // cfg3: (m + 1) x ld doubles
@@ -174,6 +210,34 @@ int main()
                 const double bytes = 2.0 * n * 8;
                 std::printf("{\"pattern\": \"strip-inplace\", \"fma_per_element\": %d, \"workgroups_per_cu\": %d, \"us\": %.1f, \"GBps\": %.0f}\n",
                             nf, bpc, med * 1e6, bytes / med / 1e9);
+            }
+        }
+    }
+    // 256-column strips (2 KB of a row per wave)
+    {
+        const long long ld = 8256, rows = 4097;
+        const int ns = (int)((ld + 255) / 256);
+        for (int bpc : {2, 3}) {
+            long long nrun = (long long)ncu * bpc / ns;
+            long long run = (rows + nrun - 1) / nrun;
+            run = (run + 3) / 4 * 4;
+            nrun = (rows + run - 1) / run;
+            for (int nf : {0, 32}) {
+                std::vector<float> ms;
+                for (int it = 0; it < 23; ++it) {
+                    CK(hipEventRecord(e0, 0));
+                    if (nf == 0) hipLaunchKernelGGL(k_strip256<0>, dim3(nrun * ns), dim3(512), 0, 0, (double *)a, ld, rows, ns, run, 1.0);
+                    else hipLaunchKernelGGL(k_strip256<32>, dim3(nrun * ns), dim3(512), 0, 0, (double *)a, ld, rows, ns, run, 1.0);
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float t = 0.f;
+                    CK(hipEventElapsedTime(&t, e0, e1));
+                    if (it >= 3) ms.push_back(t);
+                }
+                std::sort(ms.begin(), ms.end());
+                const double med = ms[ms.size() / 2] * 1e-3;
+                std::printf("{\"pattern\": \"strip256-inplace\", \"fma_per_element\": %d, \"workgroups_per_cu\": %d, \"us\": %.1f, \"GBps\": %.0f}\n",
+                            nf, bpc, med * 1e6, 2.0 * n * 8 / med / 1e9);
             }
         }
     }
