@@ -187,7 +187,7 @@ def load_traffic(path: str | None, block: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=4096)
     ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--block", type=int, default=32,
                     help="pivots deferred into one sweep of the tableau (1 = eager)")
