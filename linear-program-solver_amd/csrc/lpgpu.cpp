@@ -879,7 +879,10 @@ static int enqueue_xgroup(const Members &M, const std::vector<Args> &A, int grp,
     return launch_group_timed(h0, h0->s, A[0], grp, cnt, from_erec, 0, 1, g->dargs, (int)M.size());
 }
 
-// after a stream sync: fold recorded sweep launches into the totals
+// fold the recorded launches into the totals.  Called when the totals are
+// read (lp_update_time / lp_select_time), not at every sync, so the event
+// queries stay out of a timed pivot loop; the events of one call are all
+// complete once it has returned (its last step is a stream sync)
 static int collect_profile(lp_handle *h)
 {
     for (size_t k = 0; k + 1 < h->evused; k += 2) {
@@ -903,10 +906,7 @@ static int sync_ctl(const Members &M)
         HCHK(h, hipSetDevice(h->dev));
         HCHK(h, hipMemcpyAsync(h->hctl, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
     }
-    for (lp_handle *h : M) {
-        HCHK(h, hipStreamSynchronize(h->s));
-        CALL(collect_profile(h));
-    }
+    for (lp_handle *h : M) HCHK(h, hipStreamSynchronize(h->s));
     return LP_PIVOTED;
 }
 
@@ -1514,6 +1514,7 @@ extern "C" int lp_profile(lp_handle *h, int enable)
 
 extern "C" int lp_select_time(lp_handle *h, double *ms, int64_t *launches)
 {
+    CALL(collect_profile(h));
     *ms = h->sel_ms;
     *launches = h->sel_n;
     return LP_PIVOTED;
@@ -1521,6 +1522,7 @@ extern "C" int lp_select_time(lp_handle *h, double *ms, int64_t *launches)
 
 extern "C" int lp_update_time(lp_handle *h, double *ms, int64_t *launches)
 {
+    CALL(collect_profile(h));
     *ms = h->prof_ms;
     *launches = h->prof_n;
     return LP_PIVOTED;
