@@ -1835,7 +1835,8 @@ __device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)
     }
 }
 
-// LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt)
+// LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt,
+// 16 sc1 = write-through)
 template <int W, int RW, int NB, int LA = 0, int SA = 0>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(NB <= 32 ? 6 : 2, 8)))
 k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
@@ -2217,7 +2218,13 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, doubl
     case 25: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 2, 2); break;
     case 26: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 2); break;
     case 27: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 2, 0); break;
-    default: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 0); break;
+    case 24: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 0); break;    // plain (write-back) stores
+    case 29: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 17); break;   // sc0 sc1 stores
+    // default: sc1 (write-through) stores -- the tableau lines leave the L2
+    // as they are written instead of in the writeback at the kernel's end
+    // (sweep 104-106 vs 106.5-108.4 us per launch, 91.8-92.5k vs 91.6-91.8k
+    // pivots/s on one box)
+    default: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 16); break;
     }
 #undef SWEEP_ST_LAUNCH
 #undef SWEEP_ST_ONE

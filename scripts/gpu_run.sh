@@ -185,6 +185,14 @@ for step in "$@"; do
                 done
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_msw*.log ;;
+        wt)
+            LPGPU_SWEEP=28 run pytest_wt 300 python -u -m pytest tests/test_gpu_parity.py -k "cfg3_full and persistent" -q -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2; do
+                for V in 21 28 29; do
+                    LPGPU_SWEEP=$V run bench_wt${V}_$rep 300 python bench.py --no-cpu-baseline
+                done
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_wt*.log ;;
         tall1)
             # the whole weak-scaling tableau of N ranks on ONE GPU (rows 4096 N)
             for E in ${TALL_RANKS:-2 4 8}; do
