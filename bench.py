@@ -206,6 +206,8 @@ def main():
     ap.add_argument("--group-shards", type=int, default=0,
                     help="1-GPU diagnostic: the N-rank row-sharded job as N in-process shards "
                          "on one GPU (device copies instead of RCCL)")
+    ap.add_argument("--profile-every", type=int, default=8,
+                    help="time every k-th launch of each kernel with HIP events (1 = all)")
     ap.add_argument("--configs", action="store_true",
                     help="instead of the benchmark: cfg1/cfg2/cfg5 on GPU 0 next to the "
                          "exact-Fraction CPU path, one JSON line each")
@@ -310,7 +312,11 @@ def main():
     if done != args.warmup:
         raise SystemExit(f"warmup ended early: status {st} after {done} pivots")
     barrier()
-    eng.profile(True)
+    # kernel durations: HIP events recorded by every PROFILE_EVERY-th launch of
+    # each kernel inside the timed run (events on every launch cost ~3 % of
+    # the rate; LPGPU_BENCH_NO_EVENTS=1 times the run with none)
+    if not os.environ.get("LPGPU_BENCH_NO_EVENTS"):
+        eng.profile(True, every=args.profile_every)
     t0 = time.perf_counter()
     st, done = eng.run(_lib.RULE_STANDARD, args.steps)      # enqueue + final stream sync
     t1 = time.perf_counter()
@@ -330,9 +336,10 @@ def main():
         upd_avg_ms = upd_ms / max(upd_n, 1)
 
     lp_pps = args.steps / elapsed
+    groups = -(-args.steps // args.block)          # sweeps (and selection launches) in the run
     local_rows = (re_ - rb) + 1
     sweep_b = sweep_bytes(local_rows, n, args.block)
-    achieved = sweep_b / (upd_avg_ms * 1e-3) / 1e9
+    achieved = sweep_b / (upd_avg_ms * 1e-3) / 1e9 if upd_avg_ms > 0 else 0.0
     traffic = load_traffic(args.traffic_json, args.block) if world == 1 else None
     out = {
         "metric": METRIC,
@@ -372,7 +379,8 @@ def main():
             "traffic": traffic,
             "bytes_per_launch": sweep_b,
             "avg_launch_us": upd_avg_ms * 1e3,
-            "time_share": upd_ms / (elapsed * 1e3),
+            "time_share": upd_avg_ms * groups / (elapsed * 1e3),
+            "launches_timed": upd_n,
         },
     }
     if sel_n:
@@ -384,7 +392,8 @@ def main():
             "avg_launch_us": 1e3 * sel_ms / sel_n,
             "pivots_per_launch": args.block,
             "us_per_pivot": 1e3 * sel_ms / sel_n / args.block,
-            "time_share": sel_ms / (elapsed * 1e3),
+            "time_share": sel_ms / max(sel_n, 1) * groups / (elapsed * 1e3),
+            "launches_timed": sel_n,
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -198,9 +198,11 @@ int lp_set_block(lp_handle *h, int pivots_per_sweep);
 int lp_get_block(const lp_handle *h, int *pivots_per_sweep);
 
 /* Device-time accounting of the elimination sweep kernel (for the roofline):
- * when enabled, each sweep launch is bracketed by HIP events on the stream it
- * runs on.  lp_update_time returns the summed milliseconds and launches since
- * the last reset. */
+ * enable = 0 off, 1 every launch, k > 1 every k-th launch of each kernel
+ * (sampled: fewer events inside a timed loop).  A timed launch records HIP
+ * events on the stream it runs on, as part of the launch itself.
+ * lp_update_time returns the summed milliseconds and timed launches since the
+ * last reset. */
 int lp_profile(lp_handle *h, int enable);
 int lp_update_time(lp_handle *h, double *ms, int64_t *launches);
 /* The same for the pivot-selection launches (one per group of

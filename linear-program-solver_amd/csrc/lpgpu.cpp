@@ -76,6 +76,8 @@ struct lp_handle {
     double *xg = nullptr, *xs = nullptr, *xr = nullptr;   // sharded exchange buffers
     lp_tol tol{};
     bool prof = false;
+    int prof_every = 1;             // time every prof_every-th launch of each kind
+    int64_t prof_seen[2] = {0, 0};  // launches of each kind since lp_profile
     std::vector<hipEvent_t> ev;     // pairs (start, end) of update launches
     size_t evused = 0;
     std::vector<int> evkind;        // per pair: 0 sweep, 1 selection (k_group)
@@ -812,6 +814,7 @@ static int prof_slot(lp_handle *h, hipEvent_t *e0, hipEvent_t *e1, int kind)
 {
     *e0 = *e1 = nullptr;
     if (!h->prof) return LP_PIVOTED;
+    if (h->prof_seen[kind]++ % h->prof_every != 0) return LP_PIVOTED;   // not sampled
     if (h->evused + 2 > h->ev.size()) {
         hipEvent_t a, b;
         HCHK(h, hipEventCreate(&a));
@@ -1503,6 +1506,8 @@ extern "C" int lp_profile(lp_handle *h, int enable)
     for (lp_handle *x : members_of(h)) {
         if (!x) continue;
         x->prof = enable != 0;
+        x->prof_every = enable > 1 ? enable : 1;
+        x->prof_seen[0] = x->prof_seen[1] = 0;
         x->prof_ms = 0.0;
         x->prof_n = 0;
         x->sel_ms = 0.0;

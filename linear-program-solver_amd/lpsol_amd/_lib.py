@@ -303,8 +303,9 @@ class Engine:
         return b.value
 
     # -- timing -------------------------------------------------------------
-    def profile(self, enable: bool):
-        self.lib.lp_profile(self.h, int(bool(enable)))
+    def profile(self, enable: bool, every: int = 1):
+        """time the launches (every `every`-th of each kernel) with HIP events"""
+        self.lib.lp_profile(self.h, max(1, int(every)) if enable else 0)
 
     def update_time(self):
         """-> (total ms, launches) of the rank-1 update kernel since profile()."""
