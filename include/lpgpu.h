@@ -37,7 +37,11 @@ typedef enum lp_status {
     LP_BAD_ARG = -2,     /* ValueError / IndexError in the reference          */
     LP_DEVICE_ERROR = -3,/* HIP or RCCL failure; see lp_last_error            */
     LP_CAP_REACHED = -4, /* extension: pivot cap hit before optimality        */
-    LP_BAD_PIVOT = -5    /* ValueError('bad pivot by min ratio test') simplex.py:214-215 */
+    LP_BAD_PIVOT = -5,   /* ValueError('bad pivot by min ratio test') simplex.py:214-215 */
+    LP_OBJ_INCREASED = -6 /* AssertionError('objective value increased') simplex.py:133:
+                            a standard-rule pivot of lp_solve left the objective above
+                            its value at the start of the call by more than the stall
+                            tolerance; the solve stops after that pivot */
 } lp_status;
 
 typedef enum lp_rule {
@@ -208,6 +212,23 @@ int lp_update_time(lp_handle *h, double *ms, int64_t *launches);
 /* The same for the pivot-selection launches (one per group of
  * pivots_per_sweep pivots on the single-device path). */
 int lp_select_time(lp_handle *h, double *ms, int64_t *launches);
+
+/* Which pivot path the last lp_solve / lp_run of this handle took (extension;
+ * the reference is one process on one CPU):
+ *   LP_PATH_KERNELS     single device, per-pivot selection kernels
+ *   LP_PATH_PERSISTENT  single device, one persistent selection launch per group
+ *   LP_PATH_PEER        row-sharded, persistent selection per rank with the
+ *                       device-side peer exchange between ranks
+ *   LP_PATH_COLLECTIVE  row-sharded, per-pivot kernels + one collective
+ *                       exchange per pivot (RCCL, or the host's all-gather)
+ * A persistent group whose exchange times out (never expected: the launch is
+ * sized from the kernel's occupancy) is redone on the per-pivot kernels and
+ * counted in *fallbacks. */
+#define LP_PATH_KERNELS 0
+#define LP_PATH_PERSISTENT 1
+#define LP_PATH_PEER 2
+#define LP_PATH_COLLECTIVE 3
+int lp_exchange_path(const lp_handle *h, int *path, int *fallbacks);
 
 /* Human-readable description of the last failure on this handle (or of the
  * last failed lp_create* when h is NULL). */

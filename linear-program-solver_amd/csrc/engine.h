@@ -69,11 +69,18 @@ struct Ctl {
     double z0;           // obj_val at the start of solve (simplex.py:118)
     unsigned ticket;     // last-block ticket of k_ratio (LOCAL / CHECK modes)
     unsigned pad;
-    unsigned bar[2];     // grid-barrier counters of k_group (by group parity)
-    unsigned bar_timeout;// set if a k_group barrier gave up (never expected)
-    unsigned sel_xcc;    // XCD of the last one-XCD k_group launch (0xff: spread); a
-                         // pipelined sweep beside the next selection keeps off it
-    unsigned long long tiles[2];  // pipelined sweep: next tile (by group parity; k_group zeroes it)
+    unsigned bar[2];     // unused (kept zero)
+    unsigned bar_timeout;// set if a k_group exchange gave up (never expected)
+    unsigned pad2;
+    // k_group: the loop state at the start of the launch (every block writes
+    // the same values before any pivot of the group: a timeout is only seen
+    // by a block that ran, so the snapshot is always the failing launch's,
+    // and later launches of the batch return at once); after it the host
+    // restores it and redoes the group on the per-pivot kernels (the sweep
+    // of a timed-out group is skipped, so T still holds the group's start)
+    long long g_npiv, g_nstd, g_stuck;
+    int g_rule;
+    unsigned g_seq;      // the launch (seq) the snapshot belongs to; 0: none
 };
 
 // Per-block ratio-test summary.
@@ -125,12 +132,10 @@ struct Args {
     lp_tol tol;
     long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
     unsigned long long *gran;  // k_group summaries: 3 phases (ratio, row 0, XCD check) x GROUP_MAXBLOCKS x 8 tagged granules
-    // pipelined groups (k_group only): the previous group's pivots are not yet
-    // in T (its sweep runs concurrently); lag = 1 applies them on the fly first
-    const double *Pp;    // previous group's P (BMAX x ld)
-    const double *Mp;    // previous group's M
-    const long long *dRp;// previous group's local pivot rows
-    int lag;
+    unsigned spin_max;   // k_group: polls of one exchange before it gives up (timeout)
+    unsigned xwait_ms;   // k_group (XR): wall-clock bound of a cross-rank wait
+    int fault;           // tests only (LPGPU_FAULT): t + 1 -> block 1 withholds pivot t's ratio summary
+    int pad1;
     int rank;            // this rank (row-sharded jobs)
     // row-sharded persistent selection: this rank's exchange buffer and every
     // rank's (peer[rank] == xbuf), written by the peers over xGMI
@@ -162,90 +167,54 @@ hipError_t launch_ratio(hipStream_t s, const Args &A, int t, int grp, int mode, 
 hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
-// T_out <- A.T with the group's pivots (T_out == A.T: in place); nd_max >= ndef
+// T <- T with the group's pivots, in place; nd_max >= ndef
 // (e0, e1: events recorded at the kernel's start and end, for lp_profile)
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out,
-                        hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
-// one persistent launch selecting up to `count` chained pivots of a group;
-// seq numbers the launches of a handle (1 .. 2^24-1, then wraps to 1): it tags
-// the launch's summaries so no stale granule can match
-// xr: one rank of a row-sharded job (2: its selection may run on one XCD).
-// As (device array of nshard Args): the
-// in-process shards of one device, all in this one launch
-hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax, int lag_layout, int xr = 0,
-                        const Args *As = nullptr, int nshard = 1, hipEvent_t e0 = nullptr,
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr);
-// row-sharded: every rank writes a tagged granule to every rank's buffer and
-// waits (bounded) for all of them; *ok = 1 if all arrived (peer exchange works)
-hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev);
-int group_fits(const Args &A, int bmax, int lag_layout, int xr, int nshard);
-#ifndef LPK_GROUP_BLOCKS
-#define LPK_GROUP_BLOCKS 64
-#endif
-#ifndef LPK_GROUP_ROWS
-#define LPK_GROUP_ROWS 64
-#endif
-constexpr int GROUP_BLOCKS = LPK_GROUP_BLOCKS;   // co-resident workgroups of k_group (<= CUs) ...
+
 constexpr int GROUP_MAXBLOCKS = 256;
-constexpr int GROUP_ROWS = LPK_GROUP_ROWS;       // ... raised so a block owns at most this many rows
-constexpr int GROUP_THREADS = 64;  // one wave: block reductions stay in registers
+constexpr int GROUP_MINBLOCKS = 64;    // a small tableau still spreads its columns over 64 blocks
+constexpr int GROUP_THREADS = 64;      // one wave: block reductions stay in registers
+constexpr int GROUP_MAXRPL = 2;        // own rows per lane (<= 64 x 256 x 2 = 32768 rows per device)
 constexpr long long GROUP_LDS_MAX = 96 * 1024;
 // dynamic LDS of one k_group block: per own row / own column the pivots'
-// values at stride count + 1 (multipliers, pivot-row values; twice with a
-// lagging previous group of up to `count` pivots) + row 0 / column 0 slices
-__host__ __device__ inline long long group_lds(long long rc, long long ld, long long g, int count,
-                                               int lag)
+// values at stride count + 1 (multipliers, pivot-row values) + row 0 /
+// column 0 slices
+__host__ __device__ inline long long group_lds(long long rc, long long ld, long long g, int count)
 {
     const long long rpb = (rc + g - 1) / g, cpb = (ld + g - 1) / g;
-    return ((rpb + cpb) * (count + 1) * (lag ? 2 : 1) + cpb + rpb + 8) * 8;   // + a chunk of slack
+    return ((rpb + cpb) * (count + 1) + cpb + rpb + 8) * 8;   // + a chunk of slack
 }
-// workgroups of k_group for this shape, 0 if it does not fit (the per-pivot
-// kernels are used instead): a block owns at most GROUP_ROWS rows (one per
-// lane) and at most 4 columns per lane; a few extra blocks are taken when
-// that brings every lane down to 2 columns
-__host__ __device__ inline long long group_blocks(long long rc, long long ld, int count, int lag)
-{
-    if (ld >= 0x7fffffffLL || rc >= 0x7fffffffLL) return 0;   // indices travel as 31 bits
-    long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
-    if (g < GROUP_BLOCKS) g = GROUP_BLOCKS;
-    const long long g2 = (ld + 2 * GROUP_THREADS - 1) / (2 * GROUP_THREADS);
-    const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
-    if (g2 > g && g2 <= g + g / 8) g = g2;
-    if (g4 > g) g = g4;
-    while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX) g *= 2;
-    if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
-    if ((ld + g - 1) / g > 4 * GROUP_THREADS) return 0;   // more than 4 columns per lane
-    if ((rc + g - 1) / g > GROUP_ROWS) return 0;          // more than one row per lane
-    return group_lds(rc, ld, g, count, lag) > GROUP_LDS_MAX ? 0 : g;
-}
-// k_group workgroups when they are all to run on ONE XCD (cus = its CUs; on
-// unless LPGPU_SEL_XCD=0): at most GROUP_ROWS rows per block, at most 4
-// columns per lane, and every block co-resident on those CUs (LDS-bound).
-// 0 when the mode is off or the shape does not fit.
-inline long long group_blocks_xcd(long long rc, long long ld, int count, int cus, int lag = 0)
-{
-    static int on = -1;
-    if (on < 0) {
-        const char *v = std::getenv("LPGPU_SEL_XCD");
-        on = v ? std::atoi(v) : 1;
-    }
-    if (!on || cus <= 0 || ld >= 0x7fffffffLL || rc >= 0x7fffffffLL) return 0;
-    long long g = (rc + GROUP_ROWS - 1) / GROUP_ROWS;
-    const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
-    if (g4 > g) g = g4;
-    if (g < 1) g = 1;
-    if (g > GROUP_MAXBLOCKS) return 0;
-    // blocks per CU: LDS-bound, and at most one single-wave block per SIMD
-    // (k_group takes up to 256 VGPRs: one wave per SIMD is all that is sure)
-    long long per_cu = 160 * 1024 / (group_lds(rc, ld, g, count, lag) + 4096);   // + static LDS
-    if (per_cu > 4) per_cu = 4;
-    return per_cu >= 1 && g <= per_cu * cus ? g : 0;
-}
-// group_blocks_xcd for this device (0: the shape does not fit one XCD)
-long long group_blocks_xcd_here(long long rc, long long ld, int count, int lag);
-// can the pipelined mode's lagging selection share the device with the sweep?
-int pipeline_fits(long long rc, long long ld, int count);
+
+// Geometry of one persistent selection launch (k_group), decided on the host
+// from the compiled kernel's occupancy (group_geom, kernels.hip).  g == 0:
+// the shape does not fit (the per-pivot kernels are used instead).
+struct GroupGeom {
+    long long g = 0;     // workgroups (one wave each) per shard
+    int nr = 1;          // summaries per lane (g <= 64 nr)
+    int ipl = 2;         // own columns per lane (cpb <= 64 ipl)
+    int rpl = 1;         // own rows per lane (rpb <= 64 rpl)
+    int xmode = 0;       // 1: every block on ONE XCD (grid 8 g, blocks 0, 8, 16, ...)
+    size_t lds = 0;      // dynamic LDS per block
+    int per_cu = 0;      // resident blocks per CU the launch relies on
+};
+// rc: local constraint rows (the largest shard's for a sharded job); bmax:
+// pivots per group; xr: 0 single device, 1 row-sharded rank, 2 row-sharded
+// rank that may use one XCD; nshard: in-process shards in one launch; share:
+// processes whose launches must be resident on this device at the same time.
+GroupGeom group_geom(long long rc, long long ld, int bmax, int xr, int nshard, int share);
+// one persistent launch selecting up to `count` chained pivots of a group;
+// seq numbers the launches of a handle (1 .. 2^23-1, then wraps to 1): it tags
+// the launch's summaries so no stale granule can match.  xr: one rank of a
+// row-sharded job.  As (device array of nshard Args): the in-process shards
+// of one device, all in this one launch.  first: see k_group (call start).
+hipError_t launch_group(hipStream_t s, const Args &A, const GroupGeom &geo, int grp, int count,
+                        int from_erec, unsigned seq, int bmax, int xr, const Args *As, int nshard,
+                        int first, int fmode, int frule, long long fcap, hipEvent_t e0 = nullptr,
+                        hipEvent_t e1 = nullptr);
+// row-sharded: every rank writes a tagged granule to every rank's buffer and
+// waits (bounded) for all of them; *ok = 1 | flags OR << 1 if all arrived
+hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev);
 hipError_t launch_group_min(hipStream_t s, double *const *ptrs, int n);
 
 // per-column statistics of the local constraint rows (row 0 excluded)

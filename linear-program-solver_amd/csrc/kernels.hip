@@ -35,7 +35,10 @@
 
 #include <hip/hip_ext.h>
 
+#include <array>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 namespace lpk {
 
@@ -701,7 +704,9 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
             // min-index rule (simplex.py:123,138)
             const double z = -v;
             const double z0 = ctl->z0;
-            if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) ctl->stuck += 1;
+            const double band = A.tol.stall * fmax(1.0, fabs(z0));
+            if (z - z0 > band) ctl->status = LP_OBJ_INCREASED;   // simplex.py:133
+            if (fabs(z - z0) <= band) ctl->stuck += 1;
             else ctl->stuck = 0;
             if (ctl->stuck >= A.m + A.n) ctl->rule = LP_RULE_MIN_INDEX;
         }
@@ -747,7 +752,6 @@ typedef unsigned long long u64;
 constexpr int NRMAX = (GROUP_MAXBLOCKS + GROUP_THREADS - 1) / GROUP_THREADS;
 constexpr int NGR = 5;   // ratio summary: l (2), q (2), i
 constexpr int NGE = 8;   // row-0 summary: l (2), q (2), i, fneg | rule << 31, P[t][0] (2)
-static_assert(GROUP_ROWS <= GROUP_THREADS, "k_group: one own row per lane");
 
 __device__ __forceinline__ unsigned lo32(double d) { return (unsigned)as_ll(d); }
 __device__ __forceinline__ unsigned hi32(double d) { return (unsigned)((u64)as_ll(d) >> 32); }
@@ -786,15 +790,14 @@ __device__ __forceinline__ void publish(u64 *slot, unsigned tag, unsigned w, int
 }
 
 // every block's summary, lane l holding blocks l + 64k; polls until every
-// granule carries `tag`.  Bounded (a never-expected timeout flags the ctl).
-// every block's summary, lane l holding blocks l + 64k; polls until every
-// granule carries `tag`.  Bounded (a never-expected timeout flags the ctl).
+// granule carries `tag`.  Bounded by spin_max polls (a never-expected
+// timeout flags the ctl; the host then redoes the group, lpgpu.cpp).
 // (Keeping a second poll in flight was measured: the gather ends sooner but
 // the leftover loads delay the next phase's loads by as much -- vmcnt retires
 // in order.)
 template <int NR, int NG>
 __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[NR][NG],
-                       unsigned *timeout_flag)
+                       unsigned *timeout_flag, unsigned spin_max)
 {
     for (unsigned spins = 0;; ++spins) {
         // every load is issued before any is waited for: lanes past the last
@@ -811,7 +814,7 @@ __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[
             }
         }
         if (__all(ok)) return true;
-        if (spins > (1u << 22)) {        // seconds: never expected
+        if (spins > spin_max) {          // seconds by default: never expected
             st_sc1(timeout_flag, 1u);
             return false;
         }
@@ -891,14 +894,14 @@ __device__ __forceinline__ T ld_sys(const T *p)
 {
     return __hip_atomic_load(gp(const_cast<T *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// wall-clock bound of a cross-rank wait (the ranks' launches are enqueued by
-// different processes): 30 s of the 100 MHz real-time counter
-constexpr unsigned long long XWAIT_TICKS = 3000000000ull;
+// a cross-rank wait is bounded by wall-clock time (the ranks' launches are
+// enqueued by different processes): Args::xwait_ms of the 100 MHz real-time
+// counter (30 s by default)
 
 // NG granules of each of n slots (slot p = lane p, p < n <= 64) at stride 8
 template <int NG>
 __device__ bool gather_x(const u64 *slots, int n, unsigned tag, unsigned (&w)[NG],
-                         unsigned *timeout_flag)
+                         unsigned *timeout_flag, unsigned long long xticks)
 {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     const int p = min((int)threadIdx.x, n - 1);
@@ -911,7 +914,7 @@ __device__ bool gather_x(const u64 *slots, int n, unsigned tag, unsigned (&w)[NG
             ok = ok && (unsigned)(v >> 32) == tag;
         }
         if (__all(ok)) return true;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
             st_sc1(timeout_flag, 1u);
             return false;
         }
@@ -919,13 +922,48 @@ __device__ bool gather_x(const u64 *slots, int n, unsigned tag, unsigned (&w)[NG
     }
 }
 
+// row-0 summary of a block's own columns from per-lane values (columns
+// j = jc0 + lane + 64k; vv = INFINITY where j is not a variable column):
+// slice minimum el, first column within the tie band of el (ei, its value
+// eq), first column with c_j < -tol.cost (efn).  The first column with a
+// property is the lowest lane of the first k whose ballot is non-empty.
+template <int IPL>
+__device__ __forceinline__ void row0_summary(const double (&vv)[IPL], double vmin, long long jc0,
+                                             const lp_tol &tol, double &el, long long &ei, double &eq,
+                                             long long &efn)
+{
+    constexpr int nth = GROUP_THREADS;
+    el = wave_min(vmin);
+    efn = NONE;
+    ei = NONE;
+    eq = 0.0;
+    const double ethr = tie_band(el, tol.cost_tie);
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+        const u64 mn = __ballot(vv[k] < -tol.cost);
+        if (mn && efn == NONE) efn = jc0 + k * nth + __builtin_ctzll(mn);
+        const u64 mb = __ballot(el < INFINITY && vv[k] <= ethr);
+        if (mb && ei == NONE) {
+            const int f = __builtin_ctzll(mb);
+            ei = jc0 + k * nth + f;
+            eq = rl_d(lo32(vv[k]), hi32(vv[k]), f);
+        }
+    }
+}
+
 // NR = summaries per lane (G <= 64 NR); IPL = own columns per lane (cpb <= 64 IPL);
+// RPL = own rows per lane (rpb <= 64 RPL: lane l owns rows lr0 + l + 64k, so
+// the first row with a property is again the lowest lane of the first k);
 // XR = one rank of a row-sharded job (leaving row and pivot row exchanged
-// between ranks through the peers' exchange buffers)
-template <int NR, int IPL, bool XR>
+// between ranks through the peers' exchange buffers).
+// first (the first launch of a call): bit 0 resets the loop state (mode,
+// rule, cap = fmode, frule, fcap; k_reset's work), bit 1 loads the eager row 0
+// / column 0 from the stored tableau (k_load_eager's), bit 2 picks the first
+// entering column from the row-0 slices with one extra exchange (k_enter's).
+template <int NR, int IPL, int RPL, bool XR>
 __global__ void __launch_bounds__(GROUP_THREADS)
 k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, unsigned seq, int bmax,
-        int xmode)
+        int xmode, int first, int fmode, int frule, long long fcap)
 {
     // xmode: the grid is 8 x gper and only blocks 0, 8, 16, ... work; they
     // share one XCD under the round-robin dealing of workgroups over the 8
@@ -944,26 +982,40 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     __shared__ long long sR[BMAX + CH];     // local pivot rows of this group
     __shared__ double sPc[BMAX + CH];       // P[s][C] for the current entering column
     __shared__ double sMr[BMAX + CH];       // M[R][s] for the current leaving row
-    __shared__ long long sRp[BMAX + CH];    // previous group (lag): local pivot rows
-    __shared__ double sPcp[BMAX + CH];      //   P'[s][C]
-    __shared__ double sMrp[BMAX + CH];      //   M'[R][s]
     // dynamic LDS, per own row / own column contiguous over the pivots with an
     // odd stride cs (lanes 2-way over the banks; a chunk of pivots is one base
     // address plus immediate offsets): this block's rows' multipliers, its
-    // columns' pivot-row values, its slices of row 0 / column 0, and with a
-    // lagging previous group its multipliers and pivot-row values too.  Own
-    // data never leaves LDS for a re-read; it is also published for the other
+    // columns' pivot-row values, its slices of row 0 / column 0.  Own data
+    // never leaves LDS for a re-read; it is also published for the other
     // blocks and the sweep.
     extern __shared__ __attribute__((aligned(16))) double dyn[];
     Ctl *ctl = A.ctl;
     const unsigned G = gper, b = bid % gper;
     const int tid = threadIdx.x;
     constexpr int nth = GROUP_THREADS;
-    // this parity's previous sweep is complete (the host orders it); the
-    // other parity holds the previous group, whose sweep may still be running
-    const int np = __builtin_amdgcn_readfirstlane(A.lag ? (int)*gp(&ctl->ndef[grp ^ 1]) : 0);
+    const bool reset = (first & 1) != 0, eager = (first & 2) != 0, enter = (first & 4) != 0;
     if (b == 0 && tid == 0) *gp(&ctl->ndef[grp]) = 0;
-    if (ld_sc1(&ctl->status) != LP_PIVOTED) return;
+    // a stopped loop, or an earlier group of the batch that timed out
+    if (!reset && (ld_sc1(&ctl->status) != LP_PIVOTED || ld_sc1(&ctl->bar_timeout) != 0u)) return;
+    const long long cap = reset ? fcap : *gp(&ctl->cap);
+    const int mode = reset ? fmode : *gp(&ctl->mode);
+    // counters live in registers for the launch (block 0 publishes them)
+    long long npiv = reset ? 0 : ld_sc1(&ctl->npiv);
+    int rule = reset ? frule : ld_sc1(&ctl->rule);
+    long long nstd = 0, stuck = 0;
+    if (!reset) {
+        nstd = ld_sc1(&ctl->nstd);
+        stuck = ld_sc1(&ctl->stuck);
+    }
+    if (tid == 0) {
+        // the loop state before this group: what a timed-out group is redone
+        // from (written before anything of this launch can time out)
+        st_sc1(&ctl->g_npiv, npiv);
+        st_sc1(&ctl->g_nstd, nstd);
+        st_sc1(&ctl->g_stuck, stuck);
+        st_sc1(&ctl->g_rule, rule);
+        st_sc1(&ctl->g_seq, seq);
+    }
     u64 *grR = A.gran;                         // ratio summaries [G][8]
     u64 *grE = A.gran + GROUP_MAXBLOCKS * 8;   // row-0 summaries [G][8]
     bool fast = false;
@@ -974,7 +1026,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         u64 *grX = A.gran + 2 * GROUP_MAXBLOCKS * 8;
         if (threadIdx.x == 0) st_sc1(&grX[b * 8], ((u64)gtag(seq, 0, 7) << 32) | xcc);
         unsigned wx[NRMAX][1];
-        if (!gather<NRMAX, 1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout)) {
+        if (!gather<NRMAX, 1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
             if (b == 0 && threadIdx.x == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
             return;
         }
@@ -983,13 +1035,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         for (int k = 0; k < NRMAX; ++k)
             if (threadIdx.x + k * GROUP_THREADS < G) same = same && wx[k][0] == xcc;
         fast = __all(same);
-        if (b == 0 && threadIdx.x == 0) *gp(&ctl->sel_xcc) = fast ? xcc : 0xffu;
-    } else if (b == 0 && threadIdx.x == 0) {
-        *gp(&ctl->sel_xcc) = 0xffu;
     }
-    // this parity's pipelined sweep (after this launch) starts at tile 0
-    if (b == 0 && threadIdx.x == 0) *gp(&ctl->tiles[grp]) = 0ull;
-    const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= nth)
+    const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= RPL nth)
     const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
     const long long cpb = (A.ld + G - 1) / G;               // columns per block (<= IPL nth)
     const long long jc0 = b * cpb, jc1 = min(jc0 + cpb, A.ld);
@@ -998,65 +1045,69 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     double *lP = lM + rpb * cs;              // [cpb][cs]  P[s][own column]
     double *l0 = lP + cpb * cs;              // [cpb]      row 0 slice
     double *lc = l0 + cpb;                   // [rpb]      column 0 slice
-    double *lMp = lc + rpb;                  // [rpb][cs]  previous group (lag)
-    double *lPp = lMp + (np ? rpb * cs : 0); // [cpb][cs]
-    const long long li = lr0 + tid;          // this lane's own row
-    const bool own = li < lr1;
-    const long long kr = min((long long)tid, rpb - 1);
-    double *mrow = lM + kr * cs, *mrowp = lMp + kr * cs;
+    long long li[RPL];                       // this lane's own rows
+    bool own[RPL];
+    double *mrow[RPL];
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+        li[k] = lr0 + tid + k * nth;
+        own[k] = li[k] < lr1;
+        mrow[k] = lM + min((long long)tid + k * nth, rpb - 1) * cs;
+    }
     long long kc[IPL];                       // own columns jc0 + kc[k] (clamped into the slice)
-    const double *pcol[IPL], *pcolp[IPL];
+    const double *pcol[IPL];
 #pragma unroll
     for (int k = 0; k < IPL; ++k) {
         kc[k] = min((long long)tid + k * nth, cpb - 1);
         pcol[k] = lP + kc[k] * cs;
-        pcolp[k] = lPp + kc[k] * cs;
     }
-    for (long long j = jc0 + tid; j < jc1; j += nth) l0[j - jc0] = *gp(A.row0 + j);
-    if (own) lc[tid] = *gp(A.col0 + li);
-    u64 ownpiv = 0, ownpivp = 0;             // pivots s whose pivot row is this lane's row
-    // the lagging group's multipliers of the own row and pivot-row values of
-    // the own columns, CH pivots per round trip (every load of a chunk is
-    // issued before the first is waited for; clamped indices re-read in bounds)
-    for (int s0 = 0; s0 < np; s0 += CH) {
-        double mv[CH], pw[CH][IPL];
-        long long rv[CH];
+    // row 0 / column 0: the eager copies, or (first launch after an upload)
+    // the stored tableau's, which become the eager copies
+    for (long long j = jc0 + tid; j < jc1; j += nth) {
+        const double v = eager ? *gp(A.T + j) : *gp(A.row0 + j);
+        l0[j - jc0] = v;
+        if (eager) st_x(&A.row0[j], v, fast);
+    }
 #pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int s = min(s0 + u, np - 1);
-            mv[u] = own ? *gp(A.Mp + mi(A.rows, li, s)) : 0.0;
-            rv[u] = *gp(A.dRp + s);
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) pw[u][k] = *gp(A.Pp + s * A.ld + min(jc0 + tid + k * nth, jc1 - 1));
+    for (int k = 0; k < RPL; ++k)
+        if (own[k]) {
+            const double v = eager ? *gp(A.T + li[k] * A.ld) : *gp(A.col0 + li[k]);
+            lc[tid + k * nth] = v;
+            if (eager) st_x(&A.col0[li[k]], v, fast);
         }
-#pragma unroll
-        for (int u = 0; u < CH; ++u)
-            if (s0 + u < np) {
-                if (own) mrowp[s0 + u] = mv[u];
-#pragma unroll
-                for (int k = 0; k < IPL; ++k)
-                    if (jc0 + tid + k * nth < jc1) lPp[(tid + k * nth) * cs + s0 + u] = pw[u][k];
-                if (rv[u] == li) ownpivp |= 1ull << (s0 + u);
-            }
-    }
-    if (tid < np) sRp[tid] = *gp(A.dRp + tid);
-    const long long cap = *gp(&ctl->cap);
-    const int mode = *gp(&ctl->mode);
-    // counters live in registers for the launch (block 0 publishes them)
-    long long npiv = ld_sc1(&ctl->npiv);
-    int rule = ld_sc1(&ctl->rule);
-    long long nstd = 0, stuck = 0;
+    if (eager && b == 0 && tid == 0) st_x(&A.col0[0], *gp(A.T), fast);
     double z0 = 0.0;
+    __syncthreads();
     if (b == 0 && tid == 0) {
-        nstd = *gp(&ctl->nstd);
-        stuck = *gp(&ctl->stuck);
-        z0 = *gp(&ctl->z0);
+        if (reset) {
+            z0 = -l0[0];                     // obj_val at the start (simplex.py:118)
+            st_x(&ctl->status, (int)LP_PIVOTED, fast);
+            st_x(&ctl->mode, mode, fast);
+            st_x(&ctl->rule, rule, fast);
+            st_x(&ctl->chain, 1, fast);
+            st_x(&ctl->cap, cap, fast);
+            st_x(&ctl->r, -1LL, fast);
+            st_x(&ctl->c, -1LL, fast);
+            st_x(&ctl->npiv, 0LL, fast);
+            st_x(&ctl->nstd, 0LL, fast);
+            st_x(&ctl->stuck, 0LL, fast);
+            st_x(&ctl->z0, z0, fast);
+            st_x(&ctl->ndef[grp ^ 1], 0LL, fast);
+            // a flag left by an unrecovered earlier call (a block of this
+            // launch that times out sets it again)
+            st_sc1(&ctl->bar_timeout, 0u);
+        } else {
+            z0 = *gp(&ctl->z0);
+        }
     }
     int status = LP_PIVOTED;
     int pending = -1;                 // pivot whose column-0 update is still due
     long long pendR = -1;
     double p0 = 0.0;                  // its P[.][0]
-    __syncthreads();
+    u64 ownpiv[RPL];                  // pivots s whose pivot row is the lane's k-th row
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) ownpiv[k] = 0;
+    int stop = 0;                     // block 0: the objective increased (simplex.py:133)
     for (int tv = 0; tv < count; ++tv) {
         // the pivot index is wave-uniform; saying so keeps the chains'
         // trip counts and bounds in SGPRs (scalar branches, no exec masking:
@@ -1065,7 +1116,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         stamp(A, b, t, 0);
         // ---- entering column
         long long C;
-        if (t == 0 && !from_erec) {
+        if (t == 0 && !from_erec && !enter) {
             C = ld_sc1(&ctl->c) + 1;
         } else {
             const bool capped = cap >= 0 && npiv >= cap;
@@ -1073,7 +1124,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             long long ei[NR];
             long long ef = NONE;
             double emin = INFINITY;
-            if (t == 0) {      // previous launch's summaries (kernel boundary: plain data)
+            bool halt = false;
+            if (t == 0 && from_erec) {   // previous launch's summaries (kernel boundary: plain data)
 #pragma unroll
                 for (int k = 0; k < NR; ++k) {
                     const unsigned bb = tid + k * nth;
@@ -1091,8 +1143,34 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 }
                 rule = (int)__builtin_amdgcn_readfirstlane((int)ld_sc1(&A.erec[0].rule));
             } else {
+                const unsigned etag = t == 0 ? gtag(seq, 0, 0) : gtag(seq, t - 1, 1);
+                if (t == 0) {
+                    // first pivot of a call: every block's summary of its
+                    // row-0 slice, exchanged like a pivot's (k_enter's work)
+                    double vv[IPL], vmin = INFINITY;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        const long long j = jc0 + tid + k * nth;
+                        vv[k] = INFINITY;
+                        if (j < jc1 && j >= 1 && j <= A.n) {
+                            vv[k] = l0[kc[k]];
+                            vmin = fmin(vmin, vv[k]);
+                        }
+                    }
+                    double sel_, seq_;
+                    long long sei_, sfn_;
+                    row0_summary<IPL>(vv, vmin, jc0, A.tol, sel_, sei_, seq_, sfn_);
+                    unsigned wv = 0;
+                    if (tid == 0) wv = lo32(sel_);
+                    else if (tid == 1) wv = hi32(sel_);
+                    else if (tid == 2) wv = lo32(seq_);
+                    else if (tid == 3) wv = hi32(seq_);
+                    else if (tid == 4) wv = idx32(sei_);
+                    else if (tid == 5) wv = idx32(sfn_) & 0x7fffffffu;
+                    publish(&grE[b * 8], etag, wv, NGE, fast);
+                }
                 unsigned w[NR][NGE];
-                if (!gather<NR, NGE>(grE, G, gtag(seq, t - 1, 1), w, &ctl->bar_timeout)) {
+                if (!gather<NR, NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -1105,18 +1183,22 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     if (bb < G) {
                         el[k] = mk_d(w[k][0], w[k][1]);
                         eq[k] = mk_d(w[k][2], w[k][3]);
-                        ei[k] = un_idx(w[k][4]);
+                        ei[k] = un_idx(w[k][4] & 0x7fffffffu);
                         const long long f = un_idx(w[k][5] & 0x7fffffffu);
                         ef = f < ef ? f : ef;
                         emin = fmin(emin, el[k]);
                     }
                 }
-                // block 0's summary (lane 0) carries the rule and P[t-1][0]
-                rule = (int)((unsigned)__builtin_amdgcn_readfirstlane(w[0][5]) >> 31);
-                p0 = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
-                          __builtin_amdgcn_readfirstlane(w[0][7]));
+                if (t > 0) {
+                    // block 0's summary (lane 0) carries the rule, the stop
+                    // flag and P[t-1][0]
+                    rule = (int)((unsigned)__builtin_amdgcn_readfirstlane(w[0][5]) >> 31);
+                    halt = ((unsigned)__builtin_amdgcn_readfirstlane(w[0][4]) >> 31) != 0;
+                    p0 = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
+                              __builtin_amdgcn_readfirstlane(w[0][7]));
+                }
             }
-            if (capped) {
+            if (halt || capped) {
                 C = NONE;
             } else if (rule == LP_RULE_MIN_INDEX) {
                 C = block_min_ll(ef, sl);
@@ -1136,78 +1218,104 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     }
                 }
             }
-            if (C == NONE) status = capped ? LP_CAP_REACHED : LP_OPTIMAL;
+            if (C == NONE) status = halt ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
         stamp(A, b, t, 1);
         if (pending >= 0) {
-            if (own) {
-                const double c0 = upd(li, pendR, mrow[pending], p0, lc[tid]);
-                lc[tid] = c0;
-                st_x(&A.col0[li], c0, fast);
-            }
+#pragma unroll
+            for (int k = 0; k < RPL; ++k)
+                if (own[k]) {
+                    const double c0 = upd(li[k], pendR, mrow[k][pending], p0, lc[tid + k * nth]);
+                    lc[tid + k * nth] = c0;
+                    st_x(&A.col0[li[k]], c0, fast);
+                }
             pending = -1;
         }
         if (status != LP_PIVOTED) break;
         stamp(A, b, t, 2);
         // ---- ratio test over own rows; M[t] of own rows.  The tableau column
-        //      load is issued before the cross-block loads (one round trip).
-        double a = own ? *gp(A.T + li * A.ld + C) : 0.0;
+        //      loads are issued before the cross-block loads (one round trip).
+        double a[RPL];
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) a[k] = own[k] ? *gp(A.T + li[k] * A.ld + C) : 0.0;
         if (tid < t) sPc[tid] = ld_sc1(&A.P[tid * A.ld + C]);
-        if (tid < np) sPcp[tid] = *gp(A.Pp + tid * A.ld + C);
         if (tid == 0) {
             if (b == 0) st_x(&ctl->c, C - 1, fast);
             if (C >= jc0 && C < jc1) st_x(&A.M[mi(A.rows, 0, t)], l0[C - jc0], fast);   // row 0's multiplier
         }
         __syncthreads();
         stamp(A, b, t, 3);
-        // deferred pivots on the own row's element of column C: the previous
-        // group's (lag), then this group's 0..t-1, CH at a time.  A lane whose
-        // row was an earlier pivot row takes the select; otherwise plain FMAs.
-        auto chain_col = [&](int nt, const double *spc, const double *m, u64 piv) {
-            const u64 live = nt >= 64 ? ~0ull : (1ull << nt) - 1;
-            const bool sel = __ballot(own && (piv & live)) != 0;
-            for (int s0 = 0; s0 < nt; s0 += CH) {
-                double pc[CH], mm[CH];
+        // deferred pivots 0..t-1 on the own rows' elements of column C, CH at
+        // a time.  A lane whose row was an earlier pivot row takes the select;
+        // otherwise plain FMAs.
+        {
+            bool anyp = false;
+#pragma unroll
+            for (int k = 0; k < RPL; ++k) anyp = anyp || (own[k] && ownpiv[k] != 0);
+            const bool sel = __ballot(anyp) != 0;
+            for (int s0 = 0; s0 < t; s0 += CH) {
+                double pc[CH], mm[RPL][CH];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
-                    pc[u] = spc[s0 + u];
-                    mm[u] = m[s0 + u];
+                    pc[u] = sPc[s0 + u];
+#pragma unroll
+                    for (int k = 0; k < RPL; ++k) mm[k][u] = mrow[k][s0 + u];
                 }
                 if (!sel) {
 #pragma unroll
                     for (int u = 0; u < CH; ++u)
-                        if (s0 + u < nt) a = fma(-mm[u], pc[u], a);
+                        if (s0 + u < t) {
+#pragma unroll
+                            for (int k = 0; k < RPL; ++k) a[k] = fma(-mm[k][u], pc[u], a[k]);
+                        }
                 } else {
 #pragma unroll
                     for (int u = 0; u < CH; ++u)
-                        if (s0 + u < nt) a = ((piv >> (s0 + u)) & 1) ? pc[u] : fma(-mm[u], pc[u], a);
+                        if (s0 + u < t) {
+#pragma unroll
+                            for (int k = 0; k < RPL; ++k)
+                                a[k] = ((ownpiv[k] >> (s0 + u)) & 1) ? pc[u] : fma(-mm[k][u], pc[u], a[k]);
+                        }
                 }
             }
-        };
-        chain_col(np, sPcp, mrowp, ownpivp);
-        chain_col(t, sPc, mrow, ownpiv);
-        double qown = 0.0;
-        bool okown = false;
-        if (own) {
-            mrow[t] = a;
-            st_x(&A.M[mi(A.rows, li, t)], a, fast);
-            qown = row_ratio(a, lc[tid], A.tol, okown);
         }
-        const double lb = block_min(own && okown ? qown : INFINITY, sd);
+        double qown[RPL];
+        bool okown[RPL];
+        double mloc = INFINITY;
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            qown[k] = 0.0;
+            okown[k] = false;
+            if (own[k]) {
+                mrow[k][t] = a[k];
+                st_x(&A.M[mi(A.rows, li[k], t)], a[k], fast);
+                qown[k] = row_ratio(a[k], lc[tid + k * nth], A.tol, okown[k]);
+                okown[k] = okown[k] && own[k];
+                if (okown[k]) mloc = fmin(mloc, qown[k]);
+            }
+        }
+        const double lb = wave_min(mloc);
         stamp(A, b, t, 4);
         long long ib = NONE;
         double qb = 0.0, ab = 0.0;
         if (lb < INFINITY) {
-            // own rows are lanes in row order: the first row inside the band
-            // is the lowest lane that has one
+            // own rows are lanes in row order (per k): the first row inside
+            // the band is the lowest lane of the first k that has one
             const double thr = tie_band(lb, A.tol.ratio_tie);
-            const u64 mask = __ballot(own && okown && qown <= thr);
-            const int f = __builtin_ctzll(mask);
-            ib = lr0 + f;
-            qb = rl_d(lo32(qown), hi32(qown), f);
-            if constexpr (XR) ab = rl_d(lo32(a), hi32(a), f);
+            bool found = false;
+#pragma unroll
+            for (int k = 0; k < RPL; ++k) {
+                const u64 mask = __ballot(okown[k] && qown[k] <= thr);
+                if (!found && mask) {
+                    found = true;
+                    const int f = __builtin_ctzll(mask);
+                    ib = lr0 + k * nth + f;
+                    qb = rl_d(lo32(qown[k]), hi32(qown[k]), f);
+                    if constexpr (XR) ab = rl_d(lo32(a[k]), hi32(a[k]), f);
+                }
+            }
         }
-        {
+        if (!(A.fault == t + 1 && b == 1)) {   // fault injection (tests): block 1 never publishes
             unsigned wv = idx32(ib);
             if (tid == 0) wv = lo32(lb);
             else if (tid == 1) wv = hi32(lb);
@@ -1224,7 +1332,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         double rl[NR];
         double rmin = INFINITY;
         unsigned w[NR][NGRX];
-        if (!gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout)) {
+        if (!gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max)) {
             status = LP_DEVICE_ERROR;
             break;
         }
@@ -1279,9 +1387,9 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         }
         stamp(A, b, t, 7);
         // ---- pivot row on own columns.  prow(Rl, av): the current values of
-        //      local row Rl (stored row + this group's deferred pivots, the
-        //      lagging group's first) divided by the pivot element.  Tableau
-        //      row loads first, then the cross-block loads (one round trip).
+        //      local row Rl (stored row + this group's deferred pivots)
+        //      divided by the pivot element.  Tableau row loads first, then
+        //      the cross-block loads (one round trip).
         double pv_[IPL];                  // this pivot's normalised row on own columns
         const double f0 = ld_sc1(&A.M[mi(A.rows, 0, t)]);
         auto prow = [&](long long Rl, double avv) {
@@ -1292,37 +1400,31 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 xv[k] = j < jc1 ? *gp(A.T + Rl * A.ld + j) : 0.0;
             }
             if (tid <= t) sMr[tid] = ld_sc1(&A.M[mi(A.rows, Rl, tid)]);
-            if (tid < np) sMrp[tid] = *gp(A.Mp + mi(A.rows, Rl, tid));
             // pivots s whose pivot row is Rl: the select instead of the FMA (uniform)
             const u64 rpiv = __ballot(tid < t && sR[tid] == Rl);
-            const u64 rpivp = __ballot(tid < np && sRp[tid] == Rl);
             __syncthreads();
             stamp(A, b, t, 8);
             const double av = XR ? avv : sMr[t];
-            auto chain_row = [&](int nt, const double *smr, const double *const (&pc)[IPL], u64 piv) {
-                for (int s0 = 0; s0 < nt; s0 += CH) {
-                    double mr[CH], pv[CH][IPL];
+            for (int s0 = 0; s0 < t; s0 += CH) {
+                double mr[CH], pv[CH][IPL];
 #pragma unroll
-                    for (int u = 0; u < CH; ++u) {
-                        mr[u] = smr[s0 + u];
+                for (int u = 0; u < CH; ++u) {
+                    mr[u] = sMr[s0 + u];
 #pragma unroll
-                        for (int k = 0; k < IPL; ++k) pv[u][k] = pc[k][s0 + u];
-                    }
-#pragma unroll
-                    for (int u = 0; u < CH; ++u)
-                        if (s0 + u < nt) {
-                            if ((piv >> (s0 + u)) & 1) {     // row Rl was pivot row s
-#pragma unroll
-                                for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
-                            } else {
-#pragma unroll
-                                for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
-                            }
-                        }
+                    for (int k = 0; k < IPL; ++k) pv[u][k] = pcol[k][s0 + u];
                 }
-            };
-            chain_row(np, sMrp, pcolp, rpivp);
-            chain_row(t, sMr, pcol, rpiv);
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (s0 + u < t) {
+                        if ((rpiv >> (s0 + u)) & 1) {     // row Rl was pivot row s
+#pragma unroll
+                            for (int k = 0; k < IPL; ++k) xv[k] = pv[u][k];
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
+                        }
+                    }
+            }
             if (A.stamps) {       // diagnostic: the chain's results exist
                 asm volatile("" ::"v"(xv[0]), "v"(xv[IPL - 1]));
                 stamp(A, b, t, 12);
@@ -1347,6 +1449,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             //      normalised row: the winner's row is then already on its way.
             const int par = t & 1;
             const int N = A.nranks;
+            const unsigned long long xticks = (unsigned long long)A.xwait_ms * 100000ull;
             u64 *xs = A.xbuf + par * XS_SUM_PAR;           // local slots, written by the peers
             if (b == 0 && tid < 7) {
                 const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
@@ -1383,7 +1486,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 send_row(3);
             }
             unsigned x[7];
-            if (!gather_x<7>(xs, N, gtag(seq, t, 2), x, &ctl->bar_timeout)) {
+            if (!gather_x<7>(xs, N, gtag(seq, t, 2), x, &ctl->bar_timeout, xticks)) {
                 status = LP_DEVICE_ERROR;
                 break;
             }
@@ -1406,17 +1509,26 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 // to every rank (the straddle slot); rank ps then ships that
                 // row's normalised values instead of its candidate's
                 if (A.rank == ps) {
-                    const u64 mk = __ballot(own && okown && qown <= thr);
-                    const int fr = mk ? __builtin_ctzll(mk) : 0;
-                    const long long ir = mk ? lr0 + fr : NONE;
-                    const double ar = rl_d(lo32(a), hi32(a), fr);
+                    long long ir = NONE;
+                    double ar = 0.0;
+                    bool found = false;
+#pragma unroll
+                    for (int k = 0; k < RPL; ++k) {
+                        const u64 mk = __ballot(okown[k] && qown[k] <= thr);
+                        if (!found && mk) {
+                            found = true;
+                            const int fr = __builtin_ctzll(mk);
+                            ir = lr0 + k * nth + fr;
+                            ar = rl_d(lo32(a[k]), hi32(a[k]), fr);
+                        }
+                    }
                     u64 *loc = A.xbuf + XS_PROW + 2LL * N * XS_PROW_RANK;
                     if (tid < 3) {
                         const unsigned wv = tid == 0 ? idx32(ir) : tid == 1 ? lo32(ar) : hi32(ar);
                         st_sc1(&loc[b * 8 + tid], ((u64)gtag(seq, t, 4) << 32) | wv);
                     }
                     unsigned wl[NR][3];
-                    if (!gather<NR, 3>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout)) {
+                    if (!gather<NR, 3>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout, A.spin_max)) {
                         status = LP_DEVICE_ERROR;
                         break;
                     }
@@ -1442,7 +1554,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     }
                 }
                 unsigned y[3];
-                if (!gather_x<3>(xs + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctl->bar_timeout)) {
+                if (!gather_x<3>(xs + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctl->bar_timeout, xticks)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -1475,7 +1587,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                                     ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
                     }
                     if (__all(ok)) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > XWAIT_TICKS) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
                         st_sc1(&ctl->bar_timeout, 1u);
                         status = LP_DEVICE_ERROR;
                         break;
@@ -1487,7 +1599,9 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         } else {
             prow(R, 0.0);
         }
-        if (li == R) ownpiv |= 1ull << t;
+#pragma unroll
+        for (int k = 0; k < RPL; ++k)
+            if (li[k] == R) ownpiv[k] |= 1ull << t;
         if (tid == 0) sR[t] = R;
         double vmin = INFINITY, v0 = 0.0;
         double vv[IPL];                   // new row 0 on own columns (INFINITY: not a variable column)
@@ -1511,36 +1625,25 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         }
         __syncthreads();
         stamp(A, b, t, 9);
-        // row-0 summary of own columns, from registers: columns j = jc0 +
-        // lane + 64k, so the first column with a property is the lowest lane
-        // of the first k whose ballot is non-empty
-        const double el = block_min(vmin, sd);
-        long long efn = NONE, ei = NONE;
-        double eq = 0.0;
-        const double ethr = tie_band(el, A.tol.cost_tie);
-#pragma unroll
-        for (int k = 0; k < IPL; ++k) {
-            const u64 mn = __ballot(vv[k] < -A.tol.cost);
-            if (mn && efn == NONE) efn = jc0 + k * nth + __builtin_ctzll(mn);
-            const u64 mb = __ballot(el < INFINITY && vv[k] <= ethr);
-            if (mb && ei == NONE) {
-                const int f = __builtin_ctzll(mb);
-                ei = jc0 + k * nth + f;
-                eq = rl_d(lo32(vv[k]), hi32(vv[k]), f);
-            }
-        }
+        double el, eq;
+        long long ei, efn;
+        row0_summary<IPL>(vv, vmin, jc0, A.tol, el, ei, eq, efn);
         stamp(A, b, t, 10);
         // stall bookkeeping (simplex.py:132-137), min-index switch (:123,138)
-        // by block 0 (column 0 is in its slice: v0 = new row0[0]); the rule
-        // travels in its summary, the records are stored after the publish
+        // and the objective check (:133) by block 0 (column 0 is in its
+        // slice: v0 = new row0[0]); rule and stop flag travel in its summary,
+        // the records are stored after the publish
         if (b == 0 && tid == 0 && mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
             nstd += 1;
             const double z = -v0;
-            if (fabs(z - z0) <= A.tol.stall * fmax(1.0, fabs(z0))) stuck += 1;
+            const double band = A.tol.stall * fmax(1.0, fabs(z0));
+            if (z - z0 > band) stop = 1;   // 'objective value increased'
+            if (fabs(z - z0) <= band) stuck += 1;
             else stuck = 0;
             if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
         }
         rule = __builtin_amdgcn_readfirstlane(rule);   // block 0 lane 0 may have switched it
+        stop = __builtin_amdgcn_readfirstlane(stop);
         const double p0n = b == 0 ? lP[t] : 0.0;       // P[t][0] (column 0 is block 0's first)
         {
             unsigned wv = 0;
@@ -1548,7 +1651,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 1) wv = hi32(el);
             else if (tid == 2) wv = lo32(eq);
             else if (tid == 3) wv = hi32(eq);
-            else if (tid == 4) wv = idx32(ei);
+            else if (tid == 4) wv = (idx32(ei) & 0x7fffffffu) | ((unsigned)stop << 31);
             else if (tid == 5) wv = (idx32(efn) & 0x7fffffffu) | ((unsigned)rule << 31);
             else if (tid == 6) wv = lo32(p0n);
             else if (tid == 7) wv = hi32(p0n);
@@ -1590,116 +1693,27 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     // row-0 summary
     if (pending >= 0) {
         unsigned w[NR][NGE];
-        if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout)) {
+        if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout, A.spin_max)) {
             const double pl = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
                                    __builtin_amdgcn_readfirstlane(w[0][7]));
-            if (own) st_x(&A.col0[li], upd(li, pendR, mrow[pending], pl, lc[tid]), fast);
+#pragma unroll
+            for (int k = 0; k < RPL; ++k)
+                if (own[k]) st_x(&A.col0[li[k]], upd(li[k], pendR, mrow[k][pending], pl, lc[tid + k * nth]), fast);
         } else {
             status = LP_DEVICE_ERROR;
         }
     }
-    if (b == 0 && tid == 0 && status != LP_PIVOTED) st_sc1(&ctl->status, status);
+    if (b == 0 && tid == 0) {
+        // an increase at the launch's last pivot: nothing read the flag yet
+        if (stop && status == LP_PIVOTED) status = LP_OBJ_INCREASED;
+        if (status != LP_PIVOTED) st_sc1(&ctl->status, status);
+    }
 }
 
 // ---------------------------------------------------------------------------
-// K3: the sweep.  T_out <- T with the group's deferred pivots 0..ndef-1
-//   applied (T_out == T: in place).  Tile = 128 columns x SWEEP_ROWS rows per
-//   block of SWEEP_WAVES waves; a lane owns 2 columns (16-byte accesses) of SWEEP_RW
-//   rows, all loaded up front and held in registers while the pivots are
-//   applied in order: per pivot one LDS read of the lane's pivot-row values
-//   (the block's slice of P is staged in LDS once) and one wide scalar load
-//   of the SWEEP_RW rows' multipliers (M is pivot-major), then 2 FMAs per
-//   row.  Registers do not grow with the number of pivots, so any group size
-//   streams at the same occupancy.  Tiles holding one of the (at most ndef)
-//   pivot rows take a select per row.  Each element is loaded and stored once.
-// ---------------------------------------------------------------------------
-
-template <int SW_WAVES, int SW_RW, bool MLDS>
-__global__ void __launch_bounds__(64 * SW_WAVES)
-k_sweep(const double *T, double *Tout, const double *__restrict__ P,
-        const double *__restrict__ M, const long long *__restrict__ dR,
-        const Ctl *__restrict__ ctl, long long ld, long long rows, int grp)
-{
-    constexpr int ROWS = SW_WAVES * SW_RW;     // rows per block
-    __shared__ double2 sp[BMAX][64];          // the block's 128-column slice of P
-    __shared__ double sm[MLDS ? BMAX : 1][MLDS ? ROWS : 1];   // its rows' multipliers
-    __shared__ long long sr[BMAX];            // pivot rows
-    const int nd = (int)ctl->ndef[grp];
-    if (nd == 0) return;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long j0 = (long long)blockIdx.x * 128 + lane * 2;
-    const bool active = j0 < ld;
-    const long long base = (long long)blockIdx.y * ROWS;
-    for (int s = wave; s < nd; s += SW_WAVES)
-        sp[s][lane] = active ? *reinterpret_cast<const double2 *>(P + s * ld + j0)
-                             : make_double2(0.0, 0.0);
-    if constexpr (MLDS) {
-        // M is pivot-major: a pivot's multipliers of the block's rows are
-        // contiguous (rows past the end read the padding after M)
-        for (int idx = threadIdx.x; idx < nd * ROWS; idx += 64 * SW_WAVES) {
-            const int s = idx / ROWS, k = idx % ROWS;
-            sm[s][k] = M[s * rows + base + k];
-        }
-    }
-    if (threadIdx.x < nd) sr[threadIdx.x] = dR[threadIdx.x];
-    const long long rb = base + (long long)wave * SW_RW;
-    // rows past the end re-load the last row (in bounds) and are not stored
-    double2 x[SW_RW];
-    if (active && rb < rows) {
-#pragma unroll
-        for (int k = 0; k < SW_RW; ++k)
-            x[k] = *reinterpret_cast<const double2 *>(T + min(rb + k, rows - 1) * ld + j0);
-    }
-    __syncthreads();
-    if (!active || rb >= rows) return;
-    const long long nr = min((long long)SW_RW, rows - rb);
-    bool pivrow_here = false;
-    for (int s = 0; s < nd; ++s) {
-        const long long R = sr[s];
-        pivrow_here |= (R >= rb && R < rb + nr);
-    }
-    const double *mt = M + rb;                 // M[s * rows + rb + k]
-    auto mult = [&](int s, int k) -> double {
-        if constexpr (MLDS) return sm[s][wave * SW_RW + k];
-        else return mt[s * rows + k];
-    };
-    if (!pivrow_here) {
-#pragma unroll 2
-        for (int s = 0; s < nd; ++s) {
-            const double2 pv = sp[s][lane];
-            double fk[SW_RW];
-#pragma unroll
-            for (int k = 0; k < SW_RW; ++k) fk[k] = mult(s, k);
-#pragma unroll
-            for (int k = 0; k < SW_RW; ++k) {
-                x[k].x = fma(-fk[k], pv.x, x[k].x);
-                x[k].y = fma(-fk[k], pv.y, x[k].y);
-            }
-        }
-    } else {
-        for (int s = 0; s < nd; ++s) {
-            const double2 pv = sp[s][lane];
-            const long long kr = sr[s] - rb;   // this pivot's row in the group, if any
-#pragma unroll
-            for (int k = 0; k < SW_RW; ++k) {
-                const double fk = mult(s, k);
-                if (k == kr) {
-                    x[k] = pv;
-                } else {
-                    x[k].x = fma(-fk, pv.x, x[k].x);
-                    x[k].y = fma(-fk, pv.y, x[k].y);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < SW_RW; ++k)
-        if (k < nr) *reinterpret_cast<double2 *>(Tout + (rb + k) * ld + j0) = x[k];
-}
-
-// ---------------------------------------------------------------------------
-// K3, pipelined strip form.  A workgroup of W waves owns a 128-column strip
+// K3: the sweep (tableau.py:305-308 -> :269-289 for a whole group).  T <- T
+//   with the group's deferred pivots 0..ndef-1 applied, in place.
+//   A workgroup of W waves owns a 128-column strip
 //   (2 columns per lane, 16-byte accesses) of a contiguous run of rows; the
 //   strip's slice of P is staged in LDS ONCE for the whole run (not once per
 //   tile as in k_sweep).  Each wave walks batches of RW rows (wave w takes
@@ -1710,8 +1724,9 @@ k_sweep(const double *T, double *Tout, const double *__restrict__ P,
 //   batch's multipliers (wave-uniform) go through a per-wave LDS slot and are
 //   read as 16-byte broadcasts; no workgroup barrier after the P staging.
 //   Pivots nd..NB-1 are padding with P = 0 and multiplier 0: fma(-0, 0, x)
-//   == x for every x.  Same per-element operations and order as k_sweep:
-//   bit-identical.
+//   == x for every x.  Every element gets exactly the float64 operations of
+//   an immediate update in pivot order (upd()): bit-identical to
+//   oracle/lp_f64.c for every group size.
 // ---------------------------------------------------------------------------
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -1849,7 +1864,8 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
     __shared__ double2 sm[W][NB][RW / 2];       // per wave: the current batch's multipliers
     __shared__ long long sr[NB];
     const int nd = (int)ctl->ndef[grp];         // <= NB (the host's bound)
-    if (nd == 0) return;
+    // a group whose selection timed out is redone from its start by the host
+    if (nd == 0 || ctl->bar_timeout) return;
     // block b: strip b % nstrips of row run b / nstrips.  Consecutive blocks
     // are dealt round-robin over the 8 XCDs, so each run's multipliers and
     // each strip's slice of P are fetched into every XCD's L2 about once
@@ -1859,49 +1875,6 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
     if (r0 >= r1) return;
     if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
     sweep_strip<W, RW, NB, LA, SA>(sp, sm, sr, T, Tout, P, M, nd, ld, rows, strip, r0, r1);
-}
-
-// Pipelined sweep (out of place, beside the next group's one-XCD selection):
-// the workgroups dealt to the selection's XCD (ctl->sel_xcc, published by the
-// selection launch) leave at once, the others take tiles from a counter --
-// nbig tall row runs of run1 rows per strip first, then run2-row runs, so the
-// workgroups finish together whichever of them left.  Which XCD is avoided is
-// a speed matter only: every tile is taken exactly once either way.
-template <int W, int RW, int NB>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(6, 8)))
-k_sweep_tiles(const double *T, double *Tout, const double *__restrict__ P,
-              const double *__restrict__ M, const long long *__restrict__ dR, Ctl *ctl,
-              long long ld, long long rows, int grp, int nstrips, long long run1, long long nbig,
-              long long run2)
-{
-    static_assert(RW % 2 == 0 && NB <= BMAX && (NB * RW) % 64 == 0, "k_sweep_tiles: batch shape");
-    __shared__ double2 sp[NB][64];
-    __shared__ double2 sm[W][NB][RW / 2];
-    __shared__ long long sr[NB];
-    __shared__ long long stile;
-    const int nd = (int)ctl->ndef[grp];
-    if (nd == 0) return;
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-    if (xcc == ld_sc1(&ctl->sel_xcc)) return;   // uniform over the workgroup
-    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
-    const long long rbig = min(rows, nbig * run1);
-    const long long ntile = (long long)nstrips * (nbig + (rows - rbig + run2 - 1) / run2);
-    for (;;) {
-        __syncthreads();                        // the previous tile's LDS reads are done
-        if (threadIdx.x == 0)
-            stile = (long long)__hip_atomic_fetch_add(gp(&ctl->tiles[grp]), 1ull, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const long long k = stile;
-        if (k >= ntile) break;
-        const int strip = (int)(k % nstrips);
-        const long long q = k / nstrips;
-        const long long r0 = q < nbig ? q * run1 : rbig + (q - nbig) * run2;
-        const long long r1 = min(rows, q < nbig ? r0 + run1 : r0 + run2);
-        if (r0 < r1)
-            sweep_strip<W, RW, NB, 0, 0>(sp, sm, sr, T, Tout, P, M, nd, ld, rows, strip, r0, r1);
-    }
 }
 
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
@@ -2152,189 +2125,165 @@ static int sweep_cus()
     return ncu;
 }
 
-// The sweep: k_sweep_st (8 waves x 4-row batches, 3 workgroups per CU) in
-// place; k_sweep for the pipelined mode's out-of-place sweeps.  LPGPU_SWEEP
-// selects another shape for A/B timing (20, 22, 23: k_sweep_st; 1: k_sweep),
-// LPGPU_SWEEP_BPC the strip sweep's workgroups per CU.
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, double *T_out, hipEvent_t e0,
-                        hipEvent_t e1)
+// The sweep: k_sweep_st (8 waves x 4-row batches), write-through (sc1)
+// stores -- the tableau lines leave the L2 as they are written instead of in
+// the writeback at the kernel's end (sweep 104-106 vs 106.5-108.4 us per
+// launch at cfg3, profiles/r01/README.md).  As many row runs as fill three
+// workgroups per CU at <= 32 pivots (the strip's slice of P takes NB KB of
+// LDS: two at 48, one at 64).
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0, hipEvent_t e1)
 {
-    static int variant = -1, bpc = 0;
-    if (variant < 0) {
-        variant = 21;
-        if (const char *v = getenv("LPGPU_SWEEP")) variant = atoi(v);
-        if (const char *v = getenv("LPGPU_SWEEP_BPC")) bpc = atoi(v) > 0 ? atoi(v) : 0;
-    }
-#define SWEEP_ST_ONE(W, RW, NBV, LA, SA)                                                     \
-    hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, LA, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, T_out, \
+    constexpr int W = 8, RW = 4, SA = 16;
+    const long long ns = (A.ld + 127) / 128;
+    const int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
+    long long nrun = (long long)sweep_cus() * bpc / ns;
+    if (nrun < 1) nrun = 1;
+    long long run = (A.rows + nrun - 1) / nrun;
+    run = (run + RW - 1) / RW * RW;
+    nrun = (A.rows + run - 1) / run;
+    const dim3 grid((unsigned)(nrun * ns));
+#define SWEEP_ST_ONE(NBV)                                                                            \
+    hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, 0, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, A.T, \
                           A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
-    /* as many row runs as fill the resident capacity (BPC workgroups per CU) */
-#define SWEEP_ST_LAUNCH(W, RW, BPC, LA, SA)                                                  \
-    do {                                                                                     \
-        const long long ns = (A.ld + 127) / 128;                                             \
-        /* 48 / 64 pivots: the strip's slice of P takes 48 / 64 KB of LDS */               \
-        const int bpc_ = nd_max <= 32 ? (BPC) : nd_max <= 48 ? 2 : 1;                       \
-        long long nrun = (long long)sweep_cus() * bpc_ / ns;                                 \
-        if (nrun < 1) nrun = 1;                                                              \
-        long long run = (A.rows + nrun - 1) / nrun;                                          \
-        run = (run + (RW) - 1) / (RW) * (RW);                                                \
-        nrun = (A.rows + run - 1) / run;                                                     \
-        const dim3 grid((unsigned)(nrun * ns));                                              \
-        if (nd_max <= 16) SWEEP_ST_ONE(W, RW, 16, LA, SA);                                   \
-        else if (nd_max <= 32) SWEEP_ST_ONE(W, RW, 32, LA, SA);                              \
-        else if (nd_max <= 48) SWEEP_ST_ONE(W, RW, 48, LA, SA);                              \
-        else SWEEP_ST_ONE(W, RW, 64, LA, SA);                                                \
-    } while (0)
-    if (T_out != A.T && variant != 1) {
-        // pipelined: tiles over the CUs of the 7 XCDs the selection leaves
-        // free; tall runs (about 3/4 of the rows, one per workgroup) first,
-        // then 32-row runs to even out the end
-        constexpr int BPC = 3, RUN2 = 32;
-        const long long ns = (A.ld + 127) / 128;
-        const long long slots = (long long)sweep_cus() * 7 / 8 * BPC;
-        const long long nbig = std::max(1LL, slots / ns);
-        long long run1 = (A.rows * 3 / 4) / nbig / RUN2 * RUN2;
-        if (run1 < RUN2) run1 = RUN2;
-        const dim3 grid((unsigned)(sweep_cus() * BPC));
-#define SWEEP_TILES(NBV)                                                                      \
-    hipExtLaunchKernelGGL((k_sweep_tiles<8, 4, NBV>), grid, dim3(64 * 8), 0, s, e0, e1, 0, A.T, T_out, \
-                          A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run1, nbig, (long long)RUN2)
-        if (nd_max <= 16) SWEEP_TILES(16);
-        else SWEEP_TILES(32);
-#undef SWEEP_TILES
-        return hipGetLastError();
-    }
-    // LPGPU_SWEEP=1: the tile sweep k_sweep, also for the pipelined mode
-    const int v = T_out != A.T ? 1 : variant;
-    switch (v) {
-    case 1:
-        hipExtLaunchKernelGGL((k_sweep<16, 4, true>),
-                              dim3((unsigned)((A.ld + 127) / 128), (unsigned)((A.rows + 63) / 64)),
-                              dim3(1024), 0, s, e0, e1, 0, A.T, T_out, A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp);
-        break;
-    case 20: SWEEP_ST_LAUNCH(16, 4, bpc ? bpc : 1, 0, 0); break;
-    case 22: SWEEP_ST_LAUNCH(12, 4, bpc ? bpc : 2, 0, 0); break;
-    case 23: SWEEP_ST_LAUNCH(6, 4, bpc ? bpc : 4, 0, 0); break;
-    case 25: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 2, 2); break;
-    case 26: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 2); break;
-    case 27: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 2, 0); break;
-    case 24: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 0); break;    // plain (write-back) stores
-    case 29: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 17); break;   // sc0 sc1 stores
-    // default: sc1 (write-through) stores -- the tableau lines leave the L2
-    // as they are written instead of in the writeback at the kernel's end
-    // (sweep 104-106 vs 106.5-108.4 us per launch, 91.8-92.5k vs 91.6-91.8k
-    // pivots/s on one box)
-    default: SWEEP_ST_LAUNCH(8, 4, bpc ? bpc : 3, 0, 16); break;
-    }
-#undef SWEEP_ST_LAUNCH
+    if (nd_max <= 16) SWEEP_ST_ONE(16);
+    else if (nd_max <= 32) SWEEP_ST_ONE(32);
+    else if (nd_max <= 48) SWEEP_ST_ONE(48);
+    else SWEEP_ST_ONE(64);
 #undef SWEEP_ST_ONE
     return hipGetLastError();
 }
 
-long long group_blocks_xcd_here(long long rc, long long ld, int count, int lag)
+// ---- k_group geometry and launch ------------------------------------------
+// compiled variants (summaries per lane, columns per lane, rows per lane)
+#define GROUP_VARIANTS(X) \
+    X(1, 2, 1) X(2, 2, 1) X(4, 2, 1) X(1, 3, 1) X(2, 3, 1) X(1, 4, 1) X(2, 4, 1) X(4, 4, 1) X(4, 2, 2) X(4, 4, 2)
+
+static const void *group_kernel(int nr, int ipl, int rpl, bool xr)
 {
-    return group_blocks_xcd(rc, ld, count, sweep_cus() / 8, lag);
+#define X(NRV, IPLV, RPLV)                                                                     \
+    if (nr == NRV && ipl == IPLV && rpl == RPLV)                                               \
+        return xr ? reinterpret_cast<const void *>(&k_group<NRV, IPLV, RPLV, true>)            \
+                  : reinterpret_cast<const void *>(&k_group<NRV, IPLV, RPLV, false>);
+    GROUP_VARIANTS(X)
+#undef X
+    return nullptr;
 }
 
-// the pipelined mode's lagging one-XCD selection beside the sweep: at most two
-// blocks per CU, leaving LDS for a 16-pivot sweep workgroup next to them (a
-// full XCD -- four blocks per CU, or two of 66 KB or more -- stalled past the
-// exchange timeout in tests while the sweep ran beside it)
-int pipeline_fits(long long rc, long long ld, int count)
+// resident k_group blocks per CU the launch may rely on: the runtime's
+// occupancy answer for the compiled kernel (its VGPRs, SGPRs, static and
+// dynamic LDS), one less unless LDS is what limits it (MI355X_MICROARCH,
+// residency: the API can admit one block per CU more than the hardware does
+// at some SGPR counts; the LDS bound is exact)
+static int group_per_cu(const void *fn, size_t lds)
 {
-    const long long g = group_blocks_xcd(rc, ld, count, sweep_cus() / 8, 1);
-    if (g == 0 || g > 2LL * (sweep_cus() / 8)) return 0;
-    const long long lds = group_lds(rc, ld, g, count, 1) + 4096;
-    return 2 * lds + 20 * 1024 <= 160 * 1024 ? 1 : 0;
-}
-
-hipError_t launch_group(hipStream_t s, const Args &A, int grp, int count, int from_erec,
-                        unsigned seq, int bmax, int lag_layout, int xr, const Args *As, int nshard,
-                        hipEvent_t e0, hipEvent_t e1)
-{
-    if (xr && (lag_layout || A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
-    if (count < 1 || count > bmax || bmax > BMAX || (A.lag && !lag_layout)) return hipErrorInvalidValue;
-    // every launch of a chain must have the same geometry (the next one reads
-    // the plain per-block summaries this one leaves): sized by lag_layout
-    // a sharded job: every rank the same geometry (the column slices of block b
-    // must match across ranks), sized for the largest row block
-    const long long rcg = xr ? (A.m + A.nranks - 1) / A.nranks : A.rc;
-    long long g = 0;
-    // one-XCD selection: single device, or a rank of a sharded job whose
-    // ranks all agreed to it (xr == 2: no two ranks share a GPU)
-    const int xmode = (xr != 1 && !As) ? group_blocks_xcd(rcg, A.ld, bmax, sweep_cus() / 8, lag_layout) : 0;
-    if (xmode) g = xmode;
-    else g = group_blocks(rcg, A.ld, bmax, lag_layout);
-    if (g == 0) return hipErrorInvalidValue;
-    const size_t lds = (size_t)group_lds(rcg, A.ld, g, bmax, lag_layout);
-    const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
-    const int ipl = (int)(((A.ld + g - 1) / g + GROUP_THREADS - 1) / GROUP_THREADS);
-    const dim3 grid((unsigned)(g * (As ? nshard : 1) * (xmode ? 8 : 1)));
-#define GROUP_LAUNCH(NRV, IPLV)                                                               \
-    do {                                                                                      \
-        if (xr)                                                                               \
-            hipExtLaunchKernelGGL((k_group<NRV, IPLV, true>), grid, dim3(GROUP_THREADS), lds, s, e0, e1, 0, \
-                               A, As, (int)g, grp, count, from_erec, seq, bmax, xmode ? 1 : 0); \
-        else                                                                                  \
-            hipExtLaunchKernelGGL((k_group<NRV, IPLV, false>), grid, dim3(GROUP_THREADS), lds, s, e0, e1, 0, \
-                               A, As, (int)g, grp, count, from_erec, seq, bmax, xmode ? 1 : 0); \
-    } while (0)
-    if (ipl <= 2) {
-        if (nr <= 1) GROUP_LAUNCH(1, 2);
-        else if (nr <= 2) GROUP_LAUNCH(2, 2);
-        else GROUP_LAUNCH(NRMAX, 2);
-    } else if (ipl == 3 && nr <= 1) {   // one-XCD geometry of cfg3-like shapes (129 columns per block)
-        GROUP_LAUNCH(1, 3);
-    } else if (ipl == 3 && nr <= 2) {
-        GROUP_LAUNCH(2, 3);
-    } else {
-        if (nr <= 1) GROUP_LAUNCH(1, 4);
-        else if (nr <= 2) GROUP_LAUNCH(2, 4);
-        else GROUP_LAUNCH(NRMAX, 4);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, GROUP_THREADS, lds) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
     }
-#undef GROUP_LAUNCH
-    return hipGetLastError();
+    hipFuncAttributes at{};
+    size_t stat = 0;
+    if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+    (void)hipGetLastError();
+    const long long lds_cap = (long long)(160 * 1024) / (long long)(lds + stat);
+    return n == lds_cap ? n : n - 1;
+}
+
+static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int xr, int nshard, int share)
+{
+    GroupGeom G;
+    if (rc < 1 || ld < 1 || ld >= 0x7fffffffLL || rc >= 0x7fffffffLL || bmax < 1 || bmax > BMAX ||
+        nshard < 1 || share < 1)
+        return G;   // indices travel as 31 bits
+    static int xcd_on = -1;
+    if (xcd_on < 0) {
+        const char *v = std::getenv("LPGPU_SEL_XCD");
+        xcd_on = v ? std::atoi(v) : 1;
+    }
+    const int cus = sweep_cus(), xcd_cus = cus / 8;
+    for (int rpl = 1; rpl <= GROUP_MAXRPL; ++rpl) {
+        // at least one own row per lane-slot; every lane at most 4 columns
+        // (2 where a few extra blocks achieve it); more blocks where the LDS
+        // of one would exceed GROUP_LDS_MAX
+        long long g = (rc + 64LL * rpl - 1) / (64LL * rpl);
+        if (g < GROUP_MINBLOCKS) g = GROUP_MINBLOCKS;
+        const long long g2 = (ld + 2 * GROUP_THREADS - 1) / (2 * GROUP_THREADS);
+        const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
+        if (g2 > g && g2 <= g + g / 8) g = g2;
+        if (g4 > g) g = g4;
+        while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, bmax) > GROUP_LDS_MAX) g *= 2;
+        if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
+        const long long cpb = (ld + g - 1) / g, rpb = (rc + g - 1) / g;
+        const long long lds = group_lds(rc, ld, g, bmax);
+        if (cpb > 4 * GROUP_THREADS || rpb > (long long)rpl * GROUP_THREADS || lds > GROUP_LDS_MAX) continue;
+        int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
+        nr = nr <= 1 ? 1 : nr <= 2 ? 2 : 4;
+        int ipl = (int)((cpb + GROUP_THREADS - 1) / GROUP_THREADS);
+        ipl = ipl <= 2 ? 2 : (ipl == 3 && nr <= 2) ? 3 : 4;
+        if (rpl == 2) nr = 4;
+        const void *fn = group_kernel(nr, ipl, rpl, xr != 0);
+        if (!fn) continue;
+        const int per_cu = group_per_cu(fn, (size_t)lds);
+        if (per_cu < 1) continue;
+        G.nr = nr;
+        G.ipl = ipl;
+        G.rpl = rpl;
+        G.lds = (size_t)lds;
+        G.per_cu = per_cu;
+        // every block of every launch that waits on this one must be
+        // resident at the same time: one XCD (L2-resident hand-offs) when
+        // they fit there, else the whole device
+        if (xcd_on && xr != 1 && nshard == 1 && share == 1 && g <= (long long)per_cu * xcd_cus) {
+            G.g = g;
+            G.xmode = 1;
+            return G;
+        }
+        if (g * nshard * share <= (long long)per_cu * cus) {
+            G.g = g;
+            G.xmode = 0;
+            return G;
+        }
+    }
+    return GroupGeom{};
+}
+
+GroupGeom group_geom(long long rc, long long ld, int bmax, int xr, int nshard, int share)
+{
+    static std::mutex mu;
+    static std::map<std::array<long long, 7>, GroupGeom> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const std::array<long long, 7> key{rc, ld, bmax, xr, nshard, share, dev};
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    const GroupGeom G = group_geom_uncached(rc, ld, bmax, xr, nshard, share);
+    cache[key] = G;
+    return G;
+}
+
+hipError_t launch_group(hipStream_t s, const Args &A, const GroupGeom &geo, int grp, int count,
+                        int from_erec, unsigned seq, int bmax, int xr, const Args *As, int nshard,
+                        int first, int fmode, int frule, long long fcap, hipEvent_t e0, hipEvent_t e1)
+{
+    if (geo.g == 0 || count < 1 || count > bmax || bmax > BMAX) return hipErrorInvalidValue;
+    if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
+    const void *fn = group_kernel(geo.nr, geo.ipl, geo.rpl, xr != 0);
+    if (!fn) return hipErrorInvalidValue;
+    const int xmode = (geo.xmode && !As) ? 1 : 0;
+    const dim3 grid((unsigned)(geo.g * (As ? nshard : 1) * (xmode ? 8 : 1)));
+    Args a0 = A;
+    const Args *as = As;
+    int gper = (int)geo.g;
+    void *args[] = {&a0, &as, &gper, &grp, &count, &from_erec, &seq, &bmax,
+                    const_cast<int *>(&xmode), &first, &fmode, &frule, &fcap};
+    return hipExtLaunchKernel(fn, grid, dim3(GROUP_THREADS), args, geo.lds, s, e0, e1, 0);
 }
 
 hipError_t launch_resume(hipStream_t s, const Args &A)
 {
     hipLaunchKernelGGL(k_resume, dim3(1), dim3(1), 0, s, A.ctl);
     return hipGetLastError();
-}
-
-// can nshard shards' blocks of k_group be resident at once on this device?
-// (their blocks wait on each other; a launch that does not fit would stall)
-int group_fits(const Args &A, int bmax, int lag_layout, int xr, int nshard)
-{
-    const long long rcg = xr ? (A.m + A.nranks - 1) / A.nranks : A.rc;
-    const long long g = group_blocks(rcg, A.ld, bmax, lag_layout);
-    if (g == 0) return 0;
-    const size_t lds = (size_t)group_lds(rcg, A.ld, g, bmax, lag_layout);
-    const int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
-    const int ipl = (int)(((A.ld + g - 1) / g + GROUP_THREADS - 1) / GROUP_THREADS);
-    int per_cu = 0, dev = 0, ncu = 0;
-    hipError_t e = hipSuccess;
-#define FIT(NRV, IPLV)                                                                        \
-    e = xr ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_group<NRV, IPLV, true>,    \
-                                                          GROUP_THREADS, lds)                 \
-           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_group<NRV, IPLV, false>,   \
-                                                          GROUP_THREADS, lds)
-    if (ipl <= 2) {
-        if (nr <= 1) FIT(1, 2);
-        else if (nr <= 2) FIT(2, 2);
-        else FIT(NRMAX, 2);
-    } else {
-        if (nr <= 1) FIT(1, 4);
-        else if (nr <= 2) FIT(2, 4);
-        else FIT(NRMAX, 4);
-    }
-#undef FIT
-    if (e != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
-    // the occupancy answer can exceed what the hardware admits by one block
-    // per CU (MI355X_MICROARCH, residency): keep that margin
-    return (long long)(per_cu - 1) * ncu >= g * nshard ? 1 : 0;
 }
 
 hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev)

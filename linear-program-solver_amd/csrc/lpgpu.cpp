@@ -43,24 +43,23 @@ struct lp_handle {
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
     int block = 32;                 // pivots deferred into one sweep (1..BMAX)
-    bool persistent = true;         // single device: one k_group launch per group
+    bool persistent = true;         // one k_group launch per group where the shape fits
+    int fallbacks = 0;              // timed-out persistent groups redone on the per-pivot kernels
     long long *stamps = nullptr;    // diagnostic phase clocks (LPGPU_STAMPS=1)
     unsigned long long *gran = nullptr;  // k_group summaries (tagged granules)
     unsigned gseq = 0;              // k_group launches so far (tags their summaries)
-    // pipelined groups (single device): group g's sweep (out of place, T -> T2)
-    // runs on seven XCDs while group g+1 is selected on the eighth
-    bool pipeline = false;          // LPGPU_PIPELINE=1
-    double *T2 = nullptr;           // second tableau buffer
-    hipStream_t ssel = nullptr, ssw = nullptr;   // selection (high priority) / sweep streams
-    size_t pev_used = 0;            // events of pev handed out since the last sync
-    std::vector<hipEvent_t> pev;    // ordering events, reused per batch
+    unsigned spin_max = 1u << 22;   // polls of one k_group exchange before it gives up
+    unsigned xwait_ms = 30000;      // bound of a cross-rank wait (XR)
+    int fault_launch = 0, fault_t = 0;   // tests: LPGPU_FAULT=<launch>:<pivot>
     // row-sharded persistent selection: device-side exchange between ranks
     unsigned long long *xbuf = nullptr;     // this rank's exchange buffer (peers write it)
     unsigned long long **dpeer = nullptr;   // device table: every rank's buffer
     std::vector<void *> ipc_open;           // peer buffers opened from IPC handles
     bool peer_ok = false;                   // the exchange is set up and validated
     bool xr_xcd = false;                    // every rank on its own GPU: one-XCD selection
+    int share = 1;                          // most ranks of the job on one GPU (from the ping)
     bool peer_enable = true;                // LPGPU_PEER=0 keeps the RCCL per-pivot path
+    int last_path = 0;                      // lp_exchange_path of the last pivot loop
     hipStream_t sx = nullptr;               // in-process shards: own stream for the persistent launch
     // column scans / form checks (allocated on first use)
     lpk::ColStat *cstat = nullptr;
@@ -293,32 +292,13 @@ static Args args_of(const lp_handle *h)
     A.tol = h->tol;
     A.stamps = h->stamps;
     A.gran = h->gran;
-    A.Pp = nullptr;
-    A.Mp = nullptr;
-    A.dRp = nullptr;
-    A.lag = 0;
+    A.spin_max = h->spin_max;
+    A.xwait_ms = h->xwait_ms;
+    A.fault = 0;
+    A.pad1 = 0;
     A.rank = h->rank;
     A.xbuf = h->xbuf;
     A.peer = h->dpeer;
-    return A;
-}
-
-// arguments of a pipelined group of parity par reading tableau buffer T
-// (lag: the previous group, parity par ^ 1, is not yet swept into T)
-static Args args_par(const lp_handle *h, int par, double *T, int lag)
-{
-    Args A = args_of(h);
-    const size_t pstride = (size_t)lpk::BMAX * h->ld;
-    const size_t mstride = (size_t)lpk::BMAX * h->rows + lpk::M_PAD;
-    A.T = T;
-    A.P = h->P + par * pstride;
-    A.M = h->M + par * mstride;
-    A.dR = h->dR + par * lpk::BMAX;
-    A.dC = h->dC + par * lpk::BMAX;
-    A.Pp = h->P + (par ^ 1) * pstride;
-    A.Mp = h->M + (par ^ 1) * mstride;
-    A.dRp = h->dR + (par ^ 1) * lpk::BMAX;
-    A.lag = lag;
     return A;
 }
 
@@ -356,7 +336,9 @@ static int alloc_handle(lp_handle *h)
 {
     if (const char *sel = std::getenv("LPGPU_SELECT"))
         h->persistent = std::strcmp(sel, "kernels") != 0;
-    if (const char *pl = std::getenv("LPGPU_PIPELINE")) h->pipeline = pl[0] == '1';
+    if (const char *v = std::getenv("LPGPU_SPIN_MAX")) h->spin_max = (unsigned)std::strtoul(v, nullptr, 10);
+    if (const char *v = std::getenv("LPGPU_XWAIT_MS")) h->xwait_ms = (unsigned)std::strtoul(v, nullptr, 10);
+    if (const char *v = std::getenv("LPGPU_FAULT")) std::sscanf(v, "%d:%d", &h->fault_launch, &h->fault_t);
     if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
@@ -580,7 +562,7 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     if (!h || !h->comm || !h->xbuf) return h ? fail(h, LP_BAD_ARG, "lp_peer_handle first") : LP_BAD_ARG;
     HCHK(h, hipSetDevice(h->dev));
     std::vector<unsigned long long *> tab(h->nranks, nullptr);
-    bool shared = false;
+    int here = 1;                           // ranks of the job on this rank's GPU
     const char *all = static_cast<const char *>(handles);
     for (int p = 0; p < h->nranks; ++p) {
         if (p == h->rank) {
@@ -593,9 +575,9 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
         HCHK(h, hipIpcOpenMemHandle(&ptr, hd, hipIpcMemLazyEnablePeerAccess));
         h->ipc_open.push_back(ptr);
         tab[p] = static_cast<unsigned long long *>(ptr);
-        // a peer buffer on this very GPU: two ranks share it (tests)
+        // a peer buffer on this very GPU: the two ranks share it (tests)
         hipPointerAttribute_t at;
-        if (hipPointerGetAttributes(&at, ptr) != hipSuccess || at.device == h->dev) shared = true;
+        if (hipPointerGetAttributes(&at, ptr) != hipSuccess || at.device == h->dev) ++here;
         (void)hipGetLastError();
     }
     if (!h->dpeer) HCHK(h, hipMalloc(&h->dpeer, lpk::NRANK_MAX * sizeof(void *)));
@@ -605,9 +587,11 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     HCHK(h, hipMalloc(&dok, sizeof(int)));
     Args A = args_of(h);
     A.peer = h->dpeer;
-    // the ping also tells every rank whether any two ranks share a GPU (their
-    // one-XCD selections could then not be resident together)
-    const hipError_t e = lpk::launch_peer_ping(h->s, A, 7u, shared ? 1u : 0u, dok);
+    // the ping also carries, one-hot, how many ranks share this rank's GPU:
+    // the OR over the ranks gives every rank the same maximum (their
+    // persistent selections must then all be resident on that GPU at once)
+    const unsigned flag = 1u << (std::min(here, 8) - 1);
+    const hipError_t e = lpk::launch_peer_ping(h->s, A, 7u, flag, dok);
     if (e == hipSuccess) (void)hipMemcpyAsync(&ok, dok, sizeof(int), hipMemcpyDeviceToHost, h->s);
     const hipError_t e2 = hipStreamSynchronize(h->s);
     (void)hipFree(dok);
@@ -617,10 +601,12 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     HCHK(h, hipDeviceSynchronize());
     if (!ok) return fail(h, LP_DEVICE_ERROR, "peer exchange check timed out");
     h->peer_ok = true;
-    h->xr_xcd = (ok & 2) == 0;
-    if (const char *v = std::getenv("LPGPU_XR_XCD")) {   // A/B and tests: 0 off, 2 even if shared
+    const unsigned bits = ((unsigned)ok >> 1) & 0xffu;
+    h->share = 1;
+    while (h->share < 8 && (bits >> h->share)) ++h->share;
+    h->xr_xcd = h->share == 1;
+    if (const char *v = std::getenv("LPGPU_XR_XCD")) {   // A/B and tests: 0 off
         if (v[0] == '0') h->xr_xcd = false;
-        else if (v[0] == '2') h->xr_xcd = true;
     }
     return LP_PIVOTED;
 }
@@ -665,12 +651,6 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->dpeer) (void)hipFree(h->dpeer);
     if (h->xbuf) (void)hipFree(h->xbuf);
     if (h->sx) (void)hipStreamDestroy(h->sx);
-    if (h->ssel) (void)hipStreamSynchronize(h->ssel);
-    if (h->ssw) (void)hipStreamSynchronize(h->ssw);
-    for (hipEvent_t e : h->pev) (void)hipEventDestroy(e);
-    if (h->ssel) (void)hipStreamDestroy(h->ssel);
-    if (h->ssw) (void)hipStreamDestroy(h->ssw);
-    if (h->T2) (void)hipFree(h->T2);
     if (h->T) (void)hipFree(h->T);
     if (h->P) (void)hipFree(h->P);
     if (h->M) (void)hipFree(h->M);
@@ -830,56 +810,77 @@ static int prof_slot(lp_handle *h, hipEvent_t *e0, hipEvent_t *e1, int kind)
     return LP_PIVOTED;
 }
 
-static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, hipStream_t st = nullptr,
-                              double *T_out = nullptr)
+static int launch_sweep_timed(lp_handle *h, const Args &A, int grp)
 {
-    if (!st) st = h->s;
-    if (!T_out) T_out = A.T;
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 0));
-    HCHK(h, lpk::launch_sweep(st, A, grp, h->block, T_out, e0, e1));
+    HCHK(h, lpk::launch_sweep(h->s, A, grp, h->block, e0, e1));
     return LP_PIVOTED;
 }
 
-static int launch_group_timed(lp_handle *h, hipStream_t st, const Args &A, int grp, int cnt,
-                              int from_erec, int lag_layout, int xr = 0,
-                              const Args *As = nullptr, int nshard = 1)
+// call-start work folded into the first k_group launch of a call (k_group's
+// `first` bits): reset of the loop state, eager row 0 / column 0 after an
+// upload, the first entering column
+struct CallStart {
+    int first = 0;       // 0: not the first launch of the call
+    int mode = 0, rule = 0;
+    long long cap = -1;
+};
+
+static int launch_group_timed(lp_handle *h, const Args &A, const lpk::GroupGeom &geo, int grp, int cnt,
+                              int from_erec, int xr, const Args *As, int nshard, const CallStart &cs)
 {
     // every rank of a sharded job advances gseq identically (same calls, same order)
     h->gseq = h->gseq % ((1u << 23) - 1) + 1;   // gtag: seq * 8 * BMAX fits 32 bits
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 1));
-    HCHK(h, lpk::launch_group(st, A, grp, cnt, from_erec, h->gseq, h->block, lag_layout, xr, As,
-                              nshard, e0, e1));
+    Args a = A;
+    if (h->fault_launch > 0 && (unsigned)h->fault_launch == h->gseq) a.fault = h->fault_t + 1;
+    HCHK(h, lpk::launch_group(h->s, a, geo, grp, cnt, from_erec, h->gseq, h->block, xr, As, nshard,
+                              cs.first, cs.mode, cs.rule, cs.cap, e0, e1));
     return LP_PIVOTED;
 }
 
-static int pev_at(lp_handle *h, size_t k, hipEvent_t *e);
-
-// row-sharded persistent selection usable for this shape?  (In-process
-// shards share one device: all their blocks must fit on it at once.)
-static bool xr_ok(lp_handle *h)
+// Which pivot path a pivot loop of this handle takes (lp_exchange_path):
+//   single device: one persistent k_group launch per group where its
+//   geometry fits (occupancy of the compiled kernel), else per-pivot kernels;
+//   row-sharded: the persistent cross-rank k_group (device-side peer
+//   exchange) where the exchange is set up and every rank's launch fits on
+//   its GPU at once -- at most 4 ranks per GPU (8 processes on one GPU have
+//   more queues than the hardware scheduler keeps mapped at once, and a rank
+//   whose queue is not mapped never answers: measured, round 1) -- else one
+//   collective per pivot.  Every rank decides from the same values (global
+//   sizes, the ping's shared-GPU count), so all take the same path.
+static lpk::GroupGeom persistent_geom(lp_handle *h, const Members &M, int *xr)
 {
-    if (!h->comm || !h->peer_ok || !h->persistent) return false;
+    *xr = 0;
+    lpk::GroupGeom none;
+    if (!h->persistent) return none;
+    if (!h->comm) return lpk::group_geom(h->rc, h->ld, h->block, 0, 1, 1);
+    if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
-    if (lpk::group_blocks(rcmax, h->ld, h->block, 0) == 0) return false;
-    const Members M = members_of(h);
-    return M.size() == 1 || lpk::group_fits(args_of(h), h->block, 0, 1, (int)M.size()) != 0;
+    *xr = (M.size() == 1 && h->xr_xcd) ? 2 : 1;
+    return lpk::group_geom(rcmax, h->ld, h->block, *xr, (int)M.size(), M.size() == 1 ? h->share : 1);
 }
 
 // one persistent selection launch per rank for a group of cnt pivots.  The
 // in-process shards of one device go into ONE launch (their blocks wait on
 // each other, so all of them must be resident together).
-static int enqueue_xgroup(const Members &M, const std::vector<Args> &A, int grp, int cnt,
-                          int from_erec)
+static int enqueue_group(const Members &M, const std::vector<Args> &A, const lpk::GroupGeom &geo, int xr,
+                         int grp, int cnt, int from_erec, const CallStart &cs)
 {
-    if (M.size() == 1)
-        return launch_group_timed(M[0], M[0]->s, A[0], grp, cnt, from_erec, 0, M[0]->xr_xcd ? 2 : 1);
+    if (M.size() == 1) return launch_group_timed(M[0], A[0], geo, grp, cnt, from_erec, xr, nullptr, 1, cs);
     lp_handle *h0 = M[0];
     auto g = std::dynamic_pointer_cast<GroupComm>(h0->comm);
     if (!g) return fail(h0, LP_DEVICE_ERROR, "multi-member launch without a shard group");
-    CALL(g->stage_args(h0, A));
-    return launch_group_timed(h0, h0->s, A[0], grp, cnt, from_erec, 0, 1, g->dargs, (int)M.size());
+    std::vector<Args> As = A;
+    const unsigned next = h0->gseq % ((1u << 23) - 1) + 1;   // the seq launch_group_timed takes
+    for (size_t k = 0; k < M.size(); ++k)
+        if (M[k]->fault_launch > 0 && (unsigned)M[k]->fault_launch == next) As[k].fault = M[k]->fault_t + 1;
+    CALL(g->stage_args(h0, As));
+    // the members' launch counters advance together (their tags must match)
+    for (size_t k = 1; k < M.size(); ++k) M[k]->gseq = next;
+    return launch_group_timed(h0, A[0], geo, grp, cnt, from_erec, xr, g->dargs, (int)M.size(), cs);
 }
 
 // fold the recorded launches into the totals.  Called when the totals are
@@ -992,88 +993,53 @@ static int begin_call(const Members &M, const std::vector<Args> &A, int mode, in
 }
 
 // ---------------------------------------------------------------------------
-// pipelined groups (single device)
+// the pivot loop
 // ---------------------------------------------------------------------------
 
-// second tableau buffer and the two streams of the pipelined mode: the
-// one-XCD selection (high priority: its blocks are dispatched first) and the
-// sweep, whose workgroups keep off the selection's XCD (k_sweep_tiles)
-static int ensure_pipeline(lp_handle *h)
+// A persistent group timed out: one of its exchanges never completed (every
+// block of the launch must be resident at once -- the launch is sized from
+// the compiled kernel's occupancy, so this is never expected; a fault-
+// injection test covers it).  The failed group's sweep and every later launch
+// of the batch were skipped, so each member's stored tableau holds the state
+// at the start of the failed group.  Restore the loop state the group's
+// prologue recorded (Ctl::g_*), reload the eager row 0 / column 0 from the
+// tableau and go on with the per-pivot kernels: the same float64 operations,
+// so the results are unchanged.
+static int recover_timeout(const Members &M, const std::vector<Args> &A, int mode, int rule, int64_t cap,
+                           unsigned first_seq)
 {
-    if (h->T2 && h->ssel && h->ssw) return LP_PIVOTED;
-    HCHK(h, hipSetDevice(h->dev));
-    if (!h->T2) {
-        const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
-        HCHK(h, hipMalloc(&h->T2, tbytes));
-        HCHK(h, hipMemsetAsync(h->T2, 0, tbytes, h->s));   // padding columns stay 0
+    for (size_t k = 0; k < M.size(); ++k) {
+        lp_handle *h = M[k];
+        Ctl c = *h->hctl;
+        h->persistent = false;
+        h->fallbacks += 1;
+        h->eager_ok = false;
+        HCHK(h, lpk::launch_load_eager(h->s, A[k]));
+        h->eager_ok = true;
+        if (c.g_seq == 0 || c.g_seq == first_seq) {
+            // the call's first group: its prologue may not have run at all
+            HCHK(h, lpk::launch_reset(h->s, A[k], mode, rule, 1, cap, -1, -1));
+            c.npiv = 0;
+            c.status = LP_PIVOTED;
+        } else {
+            c.status = LP_PIVOTED;
+            c.npiv = c.g_npiv;
+            c.nstd = c.g_nstd;
+            c.stuck = c.g_stuck;
+            c.rule = c.g_rule;
+            c.bar_timeout = 0;
+            c.ndef[0] = c.ndef[1] = 0;
+            c.g_seq = 0;
+            *h->hctl = c;
+            HCHK(h, hipMemcpyAsync(h->ctl, h->hctl, sizeof(Ctl), hipMemcpyHostToDevice, h->s));
+        }
+        HCHK(h, hipStreamSynchronize(h->s));
+        h->hctl->npiv = c.npiv;
+        h->hctl->status = LP_PIVOTED;
+        h->hctl->bar_timeout = 0;
+        h->err = "a persistent selection group timed out; it was redone on the per-pivot kernels";
     }
-    int lo = 0, hi = 0;
-    HCHK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HCHK(h, hipStreamCreateWithPriority(&h->ssel, hipStreamNonBlocking, hi));
-    HCHK(h, hipStreamCreateWithPriority(&h->ssw, hipStreamNonBlocking, lo));
     return LP_PIVOTED;
-}
-
-static int pev_at(lp_handle *h, size_t k, hipEvent_t *e)
-{
-    while (h->pev.size() <= k) {
-        hipEvent_t x;
-        HCHK(h, hipEventCreateWithFlags(&x, hipEventDisableTiming));
-        h->pev.push_back(x);
-    }
-    *e = h->pev[k];
-    return LP_PIVOTED;
-}
-
-// b pivots as groups of B: selection of group g (stream ssel) overlaps the
-// sweep of group g-1 (stream ssw).  Group g reads S_{g-1} (the tableau with
-// groups < g-1 applied) and applies group g-1's pivots on the fly; the sweep
-// of group g writes S_{g+1} into the other buffer.  Returns the number of
-// groups enqueued; the caller syncs and settles the buffers (settle_buffers).
-static int enqueue_pipelined(lp_handle *h, int64_t b, bool &chained, int *ngroups)
-{
-    const int B = h->block;
-    CALL(ensure_pipeline(h));
-    double *buf[2] = {h->T, h->T2};
-    size_t ne = 0;
-    hipEvent_t e0, esel, last_sel = nullptr;
-    std::vector<hipEvent_t> esw;
-    CALL(pev_at(h, ne++, &e0));
-    HCHK(h, hipEventRecord(e0, h->s));
-    HCHK(h, hipStreamWaitEvent(h->ssel, e0, 0));
-    HCHK(h, hipStreamWaitEvent(h->ssw, e0, 0));
-    int gi = 0;
-    for (int64_t k = 0; k < b; k += B, ++gi) {
-        const int cnt = (int)std::min<int64_t>(B, b - k);
-        const int par = gi & 1;
-        Args A = args_par(h, par, buf[gi == 0 ? 0 : (gi - 1) & 1], gi > 0 ? 1 : 0);
-        if (gi >= 2) HCHK(h, hipStreamWaitEvent(h->ssel, esw[gi - 2], 0));
-        CALL(launch_group_timed(h, h->ssel, A, par, cnt, chained ? 1 : 0, 1));
-        CALL(pev_at(h, ne++, &esel));
-        HCHK(h, hipEventRecord(esel, h->ssel));
-        last_sel = esel;
-        HCHK(h, hipStreamWaitEvent(h->ssw, esel, 0));
-        Args S = args_par(h, par, buf[gi & 1], 0);
-        CALL(launch_sweep_timed(h, S, par, h->ssw, buf[(gi + 1) & 1]));
-        hipEvent_t e;
-        CALL(pev_at(h, ne++, &e));
-        HCHK(h, hipEventRecord(e, h->ssw));
-        esw.push_back(e);
-        chained = true;
-    }
-    if (last_sel) HCHK(h, hipStreamWaitEvent(h->s, last_sel, 0));
-    if (!esw.empty()) HCHK(h, hipStreamWaitEvent(h->s, esw.back(), 0));
-    *ngroups = gi;
-    return LP_PIVOTED;
-}
-
-// after the sync: groups that performed pivots were swept in order, so the
-// current tableau is S_k in buffer k & 1 (k = those groups)
-static void settle_buffers(lp_handle *h, int64_t pivots, int ngroups)
-{
-    const int B = h->block;
-    const int64_t k = std::min<int64_t>(ngroups, (pivots + B - 1) / B);
-    if (k & 1) std::swap(h->T, h->T2);
 }
 
 // Runs pivots until the device reports a status other than LP_PIVOTED or
@@ -1086,13 +1052,33 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
 {
     const Members M = members_of(h);
     std::vector<Args> A = args_all(M);
-    CALL(begin_call(M, A, mode, rule, 1, cap, -1, -1));
-    for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
+    int xr = 0;
+    lpk::GroupGeom geo = persistent_geom(h, M, &xr);
+    CallStart cs;
+    for (lp_handle *x : M) HCHK(x, hipSetDevice(x->dev));
+    if (geo.g > 0) {
+        // reset, eager copies and the first entering column happen in the
+        // first k_group launch (no k_reset / k_load_eager / k_enter launches)
+        bool eager = true;
+        for (lp_handle *x : M) eager = eager && x->eager_ok;
+        cs.first = 1 | 4 | (eager ? 0 : 2);
+        cs.mode = mode;
+        cs.rule = rule;
+        cs.cap = cap;
+        for (lp_handle *x : M) {
+            x->eager_ok = true;
+            x->hctl->r = x->hctl->c = -1;
+        }
+    } else {
+        CALL(begin_call(M, A, mode, rule, 1, cap, -1, -1));
+        for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
+    }
     const int B = h->block;
     int64_t done = 0;      // pivots performed (device count)
     int64_t batch = 8 * B;
     int grp = 0;
-    bool chained = false;  // the next pivot's entering column comes from k_prow
+    bool chained = false;  // the next pivot's entering column comes from the previous pivot
+    unsigned first_seq = 0;
     for (;;) {
         // a known pivot count goes in one batch (launches after a stop exit
         // at once); open-ended solves grow their batches
@@ -1100,31 +1086,16 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         if (limit >= 0) b = std::min<int64_t>(limit - done, std::max<int64_t>(batch, 1 << 15));
         for (lp_handle *x : M) CALL(ensure_log(x, done + b + 1));
         A = args_all(M);
-        // pipelined only where the lagging selection fits on one XCD with
-        // room to spare (the sweep has the other seven) and B <= 16
-        const bool pipelined = !h->comm && h->persistent && h->pipeline && B <= 16 &&
-                               lpk::group_blocks(h->rc, h->ld, B, 1) > 0 &&
-                               lpk::pipeline_fits(h->rc, h->ld, B) != 0;
-        int ngroups = 0;
-        const int64_t before = done;
-        h->pev_used = 0;
-        if (xr_ok(h)) {
-            // row-sharded: one persistent selection launch per rank and group,
-            // leaving row and pivot row exchanged device-side between ranks
+        const int path = geo.g > 0 ? (h->comm ? LP_PATH_PEER : LP_PATH_PERSISTENT)
+                                   : (h->comm ? LP_PATH_COLLECTIVE : LP_PATH_KERNELS);
+        for (lp_handle *x : M) x->last_path = path;
+        if (geo.g > 0) {
+            // one persistent selection launch (per rank) + one in-place sweep per group
             for (int64_t k = 0; k < b; k += B) {
                 const int cnt = (int)std::min<int64_t>(B, b - k);
-                CALL(enqueue_xgroup(M, A, grp, cnt, chained ? 1 : 0));
-                CALL(enqueue_sweep(M, A, grp));
-                grp ^= 1;
-                chained = true;
-            }
-        } else if (pipelined) {
-            CALL(enqueue_pipelined(h, b, chained, &ngroups));
-        } else if (!h->comm && h->persistent && lpk::group_blocks(h->rc, h->ld, B, 0) > 0) {
-            // one persistent selection launch + one in-place sweep per group
-            for (int64_t k = 0; k < b; k += B) {
-                const int cnt = (int)std::min<int64_t>(B, b - k);
-                CALL(launch_group_timed(h, h->s, A[0], grp, cnt, chained ? 1 : 0, 0));
+                CALL(enqueue_group(M, A, geo, xr, grp, cnt, chained ? 1 : 0, cs));
+                if (cs.first) first_seq = M[0]->gseq;
+                cs.first = 0;
                 CALL(enqueue_sweep(M, A, grp));
                 grp ^= 1;
                 chained = true;
@@ -1142,8 +1113,18 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             }
         }
         CALL(sync_ctl(M));
-        if (pipelined) settle_buffers(h, h->hctl->npiv - before, ngroups);
-        if (h->hctl->bar_timeout) return fail(h, LP_DEVICE_ERROR, "k_group summary exchange timed out");
+        bool timed_out = false;
+        for (lp_handle *x : M) timed_out = timed_out || x->hctl->bar_timeout != 0;
+        if (timed_out) {
+            if (geo.g == 0) return fail(h, LP_DEVICE_ERROR, "exchange timed out on the per-pivot path");
+            CALL(recover_timeout(M, A, mode, rule, cap, first_seq));
+            geo = lpk::GroupGeom{};
+            for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
+            chained = false;
+            grp = 0;
+            done = h->hctl->npiv;
+            continue;
+        }
         if (h->hctl->status == lpk::ST_STRADDLE) {
             // rare near-tie across ranks: the pivots before it are swept and
             // ctl->c holds its entering column; redo it with two exchanges
@@ -1350,9 +1331,18 @@ extern "C" int lp_find_pivot_max_increase(lp_handle *h, int do_pivot, int64_t *r
         best = std::max(best, inc[j]);
     }
     if (!any_neg) return LP_OPTIMAL;
-    const double lim = best - tol.ratio_tie * std::fabs(best);
-    int64_t js = 1;
-    while (!(inc[js] >= lim)) ++js;
+    // first column within the tie band of the largest increase; a non-finite
+    // largest increase (an overflowed -c_j * ratio) takes the first column
+    // that attains it
+    int64_t js = 0;
+    if (std::isfinite(best)) {
+        const double lim = best - tol.ratio_tie * std::fabs(best);
+        for (int64_t j = 1; j <= h->n && js == 0; ++j)
+            if (inc[j] >= lim) js = j;
+    }
+    for (int64_t j = 1; j <= h->n && js == 0; ++j)
+        if (inc[j] == best) js = j;
+    if (js == 0) return fail(h, LP_DEVICE_ERROR, "max-increase selection found no column");
     std::vector<double> thr(h->ld, INFINITY);
     thr[js] = band_of(cs[js].gmin, tol.ratio_tie);
     std::vector<long long> first;
@@ -1474,6 +1464,13 @@ extern "C" int lp_form_checks(lp_handle *h, int32_t *flags, int64_t *bcols)
     flags[2] = unbounded;
     flags[3] = infeasible;                                  // :510-514
     flags[4] = cs[0].nnz < h->m;                            // :516-518: some b_i == 0
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_exchange_path(const lp_handle *h, int *path, int *fallbacks)
+{
+    *path = h->last_path;
+    *fallbacks = h->fallbacks;
     return LP_PIVOTED;
 }
 

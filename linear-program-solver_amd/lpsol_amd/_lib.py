@@ -18,9 +18,16 @@ LIB_PATH = os.environ.get("LPGPU_LIB") or os.path.join(HERE, "_lib", "liblpgpu.s
 # lp_status
 PIVOTED, OPTIMAL, UNBOUNDED = 0, 1, 2
 ZERO_PIVOT, BAD_ARG, DEVICE_ERROR, CAP_REACHED, BAD_PIVOT = -1, -2, -3, -4, -5
+OBJ_INCREASED = -6
 STATUS_NAMES = {PIVOTED: "pivoted", OPTIMAL: "optimal", UNBOUNDED: "unbounded",
                 ZERO_PIVOT: "zero_pivot", BAD_ARG: "bad_arg", DEVICE_ERROR: "device_error",
-                CAP_REACHED: "cap_reached", BAD_PIVOT: "bad_pivot"}
+                CAP_REACHED: "cap_reached", BAD_PIVOT: "bad_pivot",
+                OBJ_INCREASED: "objective_increased"}
+# lp_exchange_path
+PATH_KERNELS, PATH_PERSISTENT, PATH_PEER, PATH_COLLECTIVE = 0, 1, 2, 3
+PATH_NAMES = {PATH_KERNELS: "per-pivot kernels", PATH_PERSISTENT: "persistent selection",
+              PATH_PEER: "persistent selection, device-side peer exchange",
+              PATH_COLLECTIVE: "per-pivot kernels, one collective per pivot"}
 # lp_rule
 RULE_STANDARD, RULE_MIN_INDEX = 0, 1
 
@@ -79,6 +86,7 @@ _PROTOS = {
     "lp_peer_open": (C.c_int, [_H, C.c_char_p]),
     "lp_peer_enable": (C.c_int, [_H, C.c_int]),
     "lp_set_host_allgather": (C.c_int, [_H, C.c_void_p, C.c_void_p]),
+    "lp_exchange_path": (C.c_int, [_H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "lp_last_error": (C.c_char_p, [_H]),
 }
 
@@ -292,6 +300,12 @@ class Engine:
             self._check(self.lib.lp_pivot_log(self.h, out.ctypes.data_as(_P64), cnt.value,
                                               C.byref(cnt)), self.h)
         return out
+
+    def exchange_path(self):
+        """-> (lp_exchange_path of the last solve/run, timed-out groups redone)"""
+        p, f = C.c_int(), C.c_int()
+        self.lib.lp_exchange_path(self.h, C.byref(p), C.byref(f))
+        return p.value, f.value
 
     def set_block(self, pivots_per_sweep: int):
         """pivots deferred into one sweep of the tableau (1..64)"""

@@ -17,6 +17,15 @@ L_opt = 'optimal'
 L_unb = 'unbounded'
 
 
+def optimal_row0(row0, cost_tol: float) -> bool:
+    """isOptimal of a row 0 ``[_z, c_0 .. c_{n-1}]`` with the float64
+    contract's comparison (``tableau.py:500-502``: every c_j >= 0 in exact
+    arithmetic; here c_j >= -tol.cost, the device's own 'optimal' test)."""
+    import numpy as np
+    c = np.asarray(row0, dtype=np.float64)[1:]
+    return bool(np.all(c >= -cost_tol))
+
+
 class Simplex:
     '''
     state of the simplex algorithm with canonical form tableaus and pivoting
@@ -101,17 +110,29 @@ class Simplex:
         '''
         tab = self._tab
         eng = tab._engine()
-        st, npiv, nstd = eng.solve(-1 if max_pivots is None else int(max_pivots))
+        try:
+            st, npiv, nstd = eng.solve(-1 if max_pivots is None else int(max_pivots))
+        except _lib.DeviceError:
+            tab._device_failed()
+            raise
         if npiv:
             tab._device_changed()
             self._replay(eng.log())
         self.last_solve = {'status': _lib.STATUS_NAMES.get(st, st), 'npiv': npiv, 'nstd': nstd}
         if st == _lib.UNBOUNDED:
             raise AssertionError('unbounded artificial problem (internal error)')
+        if st == _lib.OBJ_INCREASED:
+            # simplex.py:133; the offending pivot has been made, as there
+            raise AssertionError('objective value increased (internal error)')
         if st == _lib.CAP_REACHED:
             raise RuntimeError(f'pivot cap reached after {npiv} pivots')
         if st != _lib.OPTIMAL:
             raise _lib.DeviceError(f'solve ended with status {st}')
+        # simplex.py:148 -- with the float64 contract's comparison: no reduced
+        # cost below -tol.cost (the device's 'optimal' test, read back here
+        # from the device's row 0)
+        if not optimal_row0(eng.rows(0, 1)[0], eng.get_tol().cost):
+            raise AssertionError('solver failed (internal error)')
 
     def _replay(self, log):
         for r, c in log:
@@ -154,7 +175,11 @@ class Simplex:
         tab = self._tab
         if not (0 <= r < tab.getNumCons() and 0 <= c < tab.getNumVars()):
             raise IndexError('list index out of range')
-        st = tab._engine().pivot_checked(r, c)
+        try:
+            st = tab._engine().pivot_checked(r, c)
+        except _lib.DeviceError:
+            tab._device_failed()
+            raise
         if st == _lib.ZERO_PIVOT:
             raise ZeroDivisionError('Fraction(%s, 0)' % tab.getBi(r))
         if st == _lib.BAD_PIVOT:
@@ -164,7 +189,11 @@ class Simplex:
 
     def _find(self, rule: int, do_pivot: bool):
         tab = self._tab
-        res = tab._engine().find(rule, do_pivot)
+        try:
+            res = tab._engine().find(rule, do_pivot)
+        except _lib.DeviceError:
+            tab._device_failed()
+            raise
         if do_pivot and isinstance(res, tuple):
             tab._device_changed()
             self._mark(*res)
@@ -192,7 +221,11 @@ class Simplex:
         entry (:319-320); 'optimal' if there is no negative cost.
         '''
         tab = self._tab
-        res = tab._engine().find_max_increase(do_pivot)
+        try:
+            res = tab._engine().find_max_increase(do_pivot)
+        except _lib.DeviceError:
+            tab._device_failed()
+            raise
         if do_pivot and isinstance(res, tuple):
             tab._device_changed()
             self._mark(*res)

@@ -33,6 +33,14 @@ def _num(x) -> float:
     return float(Fraction(x))
 
 
+def _json_num(x) -> str:
+    """saveJson text of a float64: the simplest fraction that round-trips."""
+    x = float(x)
+    f = Fraction(x)
+    g = f.limit_denominator(1 << 20)
+    return str(g if float(g) == x else f)
+
+
 def _fmt(x: float) -> str:
     """Reference-style number text: Fractions print as 'p/q' or 'p'."""
     f = Fraction(x)
@@ -63,6 +71,7 @@ class Tableau:
     # ------------------------------------------------------------------ sync
     def _host(self) -> np.ndarray:
         """Current host mirror (downloads from the device if stale)."""
+        self._check_lost()
         if not self._host_ok:
             self._T = self._eng.download()
             self._host_ok = True
@@ -75,6 +84,7 @@ class Tableau:
 
     def _engine(self) -> _lib.Engine:
         """Device engine holding the current tableau (uploads if stale)."""
+        self._check_lost()
         if self._eng is None or (self._eng.m, self._eng.n) != (self._m, self._n):
             if self._eng is not None:
                 self._host()
@@ -92,6 +102,21 @@ class Tableau:
         """A device operation modified the tableau."""
         self._host_ok = False
         self._dev_ok = True
+
+    def _device_failed(self):
+        """A device call that changes the tableau raised DeviceError part way
+        through: the device copy can no longer be trusted.  If the host
+        mirror is current it is the state before the call (the next device
+        call re-uploads it; Simplex._bfs was not touched either); otherwise
+        the tableau is lost and every later access says so."""
+        if self._host_ok:
+            self._dev_ok = False
+        else:
+            self._lost = True
+
+    def _check_lost(self):
+        if getattr(self, '_lost', False):
+            raise _lib.DeviceError('tableau lost in an earlier device failure')
 
     def setTolerances(self, **kw):
         """Extension: float64 comparison tolerances (``lp_tol`` fields)."""
@@ -348,7 +373,11 @@ class Tableau:
         if not (0 <= r < self._m and 0 <= c < self._n):
             raise IndexError('list index out of range')
         eng = self._engine()
-        st = eng.pivot(r, c)
+        try:
+            st = eng.pivot(r, c)
+        except _lib.DeviceError:
+            self._device_failed()
+            raise
         if st == _lib.ZERO_PIVOT:
             raise ZeroDivisionError(f'zero pivot {r},{c}')
         self._device_changed()
@@ -379,15 +408,21 @@ class Tableau:
         self._host_ok, self._dev_ok = True, False
 
     def saveJson(self) -> dict[str, Any]:
+        ''' same keys and number strings as the reference (tableau.py:348-360);
+        a float64 value is written as the simplest fraction (denominator <=
+        2^20) that converts back to the same float64, else as its exact binary
+        fraction -- loadJson of the text gives back the same tableau, and
+        short rationals (the reference's own test data, 1/25, ...) print as
+        the reference prints them '''
         T = self._host()
         return {
             'm': self._m, 'n': self._n,
-            'z': str(Fraction(T[0, 0])),
-            'c': [str(Fraction(x)) for x in T[0, 1:]],
-            'b': [str(Fraction(x)) for x in T[1:, 0]],
-            'a': [[str(Fraction(x)) for x in row] for row in T[1:, 1:]],
-            'cl': self._cl,
-            'cm': self._cm,
+            'z': _json_num(T[0, 0]),
+            'c': [_json_num(x) for x in T[0, 1:]],
+            'b': [_json_num(x) for x in T[1:, 0]],
+            'a': [[_json_num(x) for x in row] for row in T[1:, 1:]],
+            'cl': list(self._cl),
+            'cm': list(self._cm),
         }
 
     def printGrid(self, labels: bool = True, rownums: bool = True,

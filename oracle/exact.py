@@ -218,6 +218,12 @@ class Unbounded(AssertionError):
     pass
 
 
+class ObjectiveIncreased(AssertionError):
+    """simplex.py:133: a standard-rule pivot of solve() raised the objective
+    above its value at the start of the call (possible only on a tableau
+    whose b has negative entries: the ratio test then picks a negative ratio)."""
+
+
 def solve(T, cap: int | None = None, log: list | None = None) -> dict:
     """Standard-rule pivots until ``steps_stuck`` reaches m+n, then min-index
     pivots to optimality (``simplex.py:116-148``).
@@ -247,7 +253,10 @@ def solve(T, cap: int | None = None, log: list | None = None) -> dict:
         pivot(T, *res)
         seq.append(res)
         nstd += 1
-        stuck = stuck + 1 if objective(T) == obj_val else 0
+        z = objective(T)
+        if z > obj_val:                       # simplex.py:133
+            raise ObjectiveIncreased("objective value increased (internal error)")
+        stuck = stuck + 1 if z == obj_val else 0
     while True:
         if cap is not None and len(seq) >= cap:
             return {"status": "cap", "npiv": len(seq), "nstd": nstd, "seq": seq}

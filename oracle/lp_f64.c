@@ -32,7 +32,9 @@
  *   ratio test         : rows with a_ic > tol.pivot; num = |b_i| <= tol.zero ? 0 : b_i
  *                        q_i = num / a_ic; g = min q; r = first i with
  *                        q_i <= g + tol.ratio_tie*|g|
- *   stall (solve)      : |z - z0| <= tol.stall * max(1, |z0|)
+ *   stall (solve)      : |z - z0| <= tol.stall * max(1, |z0|); z - z0 above
+ *                        that band stops the solve with LP_OBJ_INCREASED
+ *                        (simplex.py:133 asserts z <= obj_val)
  *   max increase       : over columns with c_j < -tol.cost: g_j = min ratio of
  *                        the column (ratio test above); 'unbounded' if any such
  *                        column has no row with a > tol.pivot (the reference
@@ -165,7 +167,9 @@ int lpf_solve(double *T, int64_t m, int64_t n, int64_t ld, const lp_tol *tol,
         if (rule == LP_RULE_STANDARD) {
             ++*nstd;
             const double z = -T[0];
-            if (fabs(z - z0) <= tol->stall * fmax(1.0, fabs(z0))) ++stuck;
+            const double band = tol->stall * fmax(1.0, fabs(z0));
+            if (z - z0 > band) return LP_OBJ_INCREASED;   /* simplex.py:133, after the pivot */
+            if (fabs(z - z0) <= band) ++stuck;
             else stuck = 0;
         }
     }

@@ -17,7 +17,9 @@ run() {
 }
 for step in "$@"; do
     case "$step" in
-        pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider ;;
+        pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        drv) run bench_drv 300 python bench.py --steps 20 --warmup 5 ;;
+        cfg4) run bench_cfg4 600 python bench.py --no-cpu-baseline --emulate-ranks 8 --steps 256 ;;
         pytestx) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;

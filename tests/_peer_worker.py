@@ -28,8 +28,10 @@ def main():
     T = gen.tableau(kind, m, ns, 31)
     m, n = T.shape[0] - 1, T.shape[1] - 1
     e = _lib.create_sharded(m, n, rank, world, None, device=0)
-    if mode in ("scan", "host"):
-        e.set_host_allgather(_lib.gloo_allgather())
+    # the host all-gather carries the per-pivot exchanges where the
+    # persistent cross-rank selection is not used (host mode; more than four
+    # ranks on one GPU) and the column scans
+    e.set_host_allgather(_lib.gloo_allgather())
     if mode != "host":
         hs = [None] * world
         dist.all_gather_object(hs, e.peer_handle())
@@ -41,6 +43,12 @@ def main():
     o = F64Tableau(T, {"ratio_tie": tie})
     ost, olog = o.run(0, k)
     assert e.log().tolist() == olog.tolist(), (rank, e.log().tolist()[:5], olog.tolist()[:5])
+    # which path ran: the persistent cross-rank selection with up to four
+    # ranks on the one GPU, one collective per pivot beyond (lpgpu.cpp,
+    # persistent_geom) or without the peer exchange
+    path, fallbacks = e.exchange_path()
+    want = _lib.PATH_PEER if mode != "host" and world <= 4 else _lib.PATH_COLLECTIVE
+    assert (path, fallbacks) == (want, 0), (rank, path, fallbacks)
     b, c = e.row_begin, e.row_count
     assert np.array_equal(e.rows(0, 1), o.T[:1])
     assert np.array_equal(e.rows(1 + b, c), o.T[1 + b:1 + b + c])

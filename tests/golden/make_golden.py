@@ -4,6 +4,7 @@ package ``lpsol``) in the build container.
 Run from the repo root (needs /root/reference, read-only):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--big]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --extra   # r2.json only
 
 It imports the reference, drives its own ``Tableau``/``Simplex`` on inputs
 from this repo's generator (``lpsol_amd.generators``) or on hand-built LPs,
@@ -259,10 +260,82 @@ def kat_fixture():
                       [[fs(x) for x in r] for r in after2]]}
 
 
+def raises_fixture(name, rows, new_b):
+    """Simplex(tab) on a canonical tableau, then setB(new_b) with a negative
+    entry and solve(): the reference's solve() asserts (simplex.py:133 /
+    :125).  Records the pivots made before the assertion, the exception and
+    the tableau it leaves."""
+    t = ref_tableau_from_rows(rows)
+    log = []
+    s = LoggingSimplex(t, log)
+    k0 = len(log)
+    t.setB([Fraction(x) for x in new_b])
+    fx = {"name": name, "mode": "raises",
+          "start": [[fs(x) for x in r] for r in rows], "new_b": [str(x) for x in new_b]}
+    try:
+        s.solve()
+        fx["error"] = None
+    except AssertionError as ex:
+        fx["error"] = type(ex).__name__
+        fx["message"] = str(ex)
+    fx["seq"] = [[r, c] for r, c, _ in log[k0:]]
+    fx["final"] = [[fs(x) for x in r] for r in ref_rows(t)]
+    print(f"{name}: {fx['error']} {fx.get('message')} after {len(fx['seq'])} pivots", flush=True)
+    return fx
+
+
+def json_fixture(name, spec):
+    """Tableau.saveJson() of the reference before and after Simplex(t).solve()
+    (tableau.py:322-360), with variable names and the basis marks."""
+    T, rows = source_of(spec)
+    t = ref_tableau_from_rows(rows)
+    before = t.saveJson()
+    s = Simplex(t)
+    s.solve()
+    after = t.saveJson()
+    dyadic = all(Fraction(x).denominator & (Fraction(x).denominator - 1) == 0
+                 for x in [after["z"]] + after["c"] + after["b"] + [v for r in after["a"] for v in r])
+    print(f"{name}: saveJson {after['m']}x{after['n']} dyadic={dyadic}", flush=True)
+    return {"name": name, "mode": "json", **spec, "before": before, "after": after,
+            "dyadic": dyadic, "bfs": list(s.getBasicSequence()), "objective": fs(s.getObjValue())}
+
+
+def extra_main():
+    """tests/golden/r2.json: solve() assertions and saveJson round trips."""
+    out = {"raises": [], "json": []}
+    # canonical 2 x 4 (slack basis); b_1 made negative: the ratio test picks
+    # row 1 (ratio -1) and the objective rises to 1 (simplex.py:133)
+    base = exact.from_strings("0", ["-1", "-1", "0", "0"], ["2", "3"],
+                              [["1", "1", "1", "0"], ["1", "2", "0", "1"]])
+    out["raises"].append(raises_fixture("obj_increase_2x4", base, ["2", "-1"]))
+    # a larger one: the assertion after a few ordinary pivots
+    T, rows = source_of({"gen": {"kind": "pos", "m": 6, "ns": 6, "seed": 5}})
+    nb = [str(x) for x in [rows[i][0] for i in range(1, 7)]]
+    nb[4] = "-1/64"
+    out["raises"].append(raises_fixture("obj_increase_pos6_s5", rows, nb))
+    z, c, b, a = gen.beale_exact()
+    out["json"].append(json_fixture("json_beale", {"exact": {"z": z, "c": c, "b": b, "a": a}}))
+    out["json"].append(json_fixture("json_kat", {"exact": {
+        "z": "0", "c": ["-40", "-30", "0", "0"], "b": ["12", "16"],
+        "a": [["1", "1", "1", "0"], ["2", "1", "0", "1"]]}}))
+    for seed in (1, 2, 3):
+        out["json"].append(json_fixture(f"json_cfg1_mixed_s{seed}",
+                                        {"gen": {"kind": "mixed", "m": 8, "ns": 10, "seed": seed}}))
+    out["json"].append(json_fixture("json_pos_12x12_s4", {"gen": {"kind": "pos", "m": 12, "ns": 12, "seed": 4}}))
+    out["json"].append(json_fixture("json_km_deg_d6", {"array": gen.klee_minty(6, True).tolist()}))
+    with open(os.path.join(OUT, "r2.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
+    ap.add_argument("--extra", action="store_true",
+                    help="only tests/golden/r2.json (solve assertions, saveJson round trips)")
     args = ap.parse_args()
+    if args.extra:
+        extra_main()
+        return
 
     small = {"kat": [kat_fixture()], "solve": [], "standard_k": [], "selection": [], "phase1": []}
     z, c, b, a = gen.beale_exact()

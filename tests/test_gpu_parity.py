@@ -45,15 +45,19 @@ def _initial_basis(T):
     return bc
 
 
-@pytest.fixture(params=["pipelined", "persistent", "kernels"])
+@pytest.fixture(params=["persistent", "kernels"])
 def select_mode(request, monkeypatch):
-    """single-device selection path: persistent k_group launches whose sweeps
-    run concurrently on their own CUs (default), the same with in-place sweeps
-    after each group, or the per-pivot k_ratio/k_prow launches (the sharded
-    path's kernels)"""
+    """single-device selection path: one persistent k_group launch per group
+    followed by the in-place sweep (default), or the per-pivot k_ratio/k_prow
+    launches (the sharded path's kernels)"""
     monkeypatch.setenv("LPGPU_SELECT", "kernels" if request.param == "kernels" else "persistent")
-    monkeypatch.setenv("LPGPU_PIPELINE", "1" if request.param == "pipelined" else "0")
     return request.param
+
+
+def no_fallback(e):
+    """the run took no timed-out persistent group (each is redone on the
+    per-pivot kernels: correct, but never expected)"""
+    assert e.exchange_path()[1] == 0
 
 
 def engine_of(T, block=8):
@@ -198,8 +202,9 @@ def test_optimal_at_start_and_cap():
     ("tall", 1, 1, 3), ("mixed", 1, 5, 3), ("mixed", 3, 60, 10), ("tall", 5, 63, 10),
     ("tall", 257, 64, 30), ("mixed", 300, 191, 30), ("tall", 513, 7, 20),
     ("tall", 1000, 2, 10), ("tall", 2, 5000, 10), ("mixed", 255, 129, 40),
-    # past the persistent kernel's limits: > 256 blocks x 64 rows, > 256 x 256 columns
-    ("tall", 16500, 3, 12), ("tall", 2, 66000, 6),
+    # two rows per lane (> 256 blocks x 64 rows), the 32768-row limit, past it
+    # (per-pivot kernels), past 256 x 256 columns
+    ("tall", 16500, 3, 12), ("tall", 32768, 9, 8), ("tall", 32769, 3, 6), ("tall", 2, 66000, 6),
 ])
 @pytest.mark.parametrize("block", [1, 7, 32, 48])
 def test_ragged_shapes_bit_exact(kind, m, ns, k, block, select_mode):
@@ -210,6 +215,7 @@ def test_ragged_shapes_bit_exact(kind, m, ns, k, block, select_mode):
     ost, olog = o.run(0, k)
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), o.T)
+    no_fallback(e)
 
 
 @pytest.mark.parametrize("block", [1, 32, 44, 64])
@@ -390,6 +396,7 @@ def test_one_xcd_selection_at_lds_edge(ns):
     ost, olog = o.run(0, 40)
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), o.T)
+    no_fallback(e)
     e.close()
 
 
@@ -406,4 +413,5 @@ def test_one_xcd_selection_block_count(m, ns, block, select_mode):
     ost, olog = o.run(0, 48)
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), o.T)
+    no_fallback(e)
     e.close()
