@@ -1,32 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark of the dense simplex pivot hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4|cfg3]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-One "step" = one simplex pivot (entering scan, ratio test, rank-1 update of
-the whole float64 tableau) with the standard rule, all on the device (the
-rank-1 updates of 32 pivots are applied in one sweep; bit-identical).
-Workload (weak scaling): every GPU holds 4096 constraint rows
-of an 8192-variable tableau.
-  N = 1 : cfg3, G_mixed(m=4096, ns=4096, seed 3) -> a 4097 x 8193 tableau
-  N > 1 : G_tall(m=4096*N, n=8192, seed 3), rows sharded 4096 per rank
-          (N = 8 is cfg4, the 32768 x 8192 tableau).  Per pivot the ranks
-          exchange candidates and the pivot row device-side (peer stores over
-          xGMI inside one persistent selection kernel per group); RCCL
-          collectives per pivot if that exchange cannot be set up.
-``value`` = pivots/s x N (each pivot sweeps N shards of 4096 x 8192), i.e.
-plain LP pivots/s at N = 1; ``lp_pivots_per_s`` is the LP-level rate.
+A pivot is the reference's ``findPivotStandard(True)``: entering-column scan,
+min-ratio test and the rank-1 elimination of the whole float64 tableau
+(``lpsol/simplex.py:251-284``, ``lpsol/tableau.py:295-308``).  The engine
+selects ``block`` pivots (default 32) from current values and then applies
+their eliminations to the stored tableau in ONE pass (bit-identical to
+immediate updates).  One STEP is one such group: ``block`` pivots selected
+plus one elimination pass over the whole tableau, so ``--steps K`` times
+K x block pivots.  ``value`` is LP pivots per second of the whole job.
 
-Inputs are resident in HBM before the timed region.  Every sweep and
-selection launch inside the timed region carries a pair of HIP events that
-the launch itself records at the kernel's start and end (hipExtLaunchKernelGGL
-on the engine's stream, lp_profile): the roofline's achieved bandwidth is the
-sweep's algorithmic bytes over that kernel time.
+Workload (BASELINE.json config 4): cfg4, the 32768 x 8192
+G_tall tableau (seed 3), STRONG scaling -- the same tableau at every N, its
+constraint rows split into N contiguous row blocks, one per GPU (row 0
+replicated).  At N = 1 the line also carries ``cfg3``: the 4096 x 8192
+G_mixed tableau (config 3, the north star's 60 %-of-HBM-roofline case)
+measured the same way.  ``--workload cfg3`` makes cfg3 the main workload.
+
+Inputs are resident in HBM before the timed region.  Every 8th sweep and
+selection launch inside the timed region records a pair of HIP events at the
+kernel's start and end (hipExtLaunchKernelGGL on the engine's stream); the
+roofline's achieved bandwidth is the sweep's algorithmic bytes over that
+kernel time.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -43,82 +46,110 @@ from lpsol_amd import generators as gen  # noqa: E402
 
 METRIC = "pivots/sec + achieved HBM GB/s on dense float64 tableau, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-ROWS_PER_GPU = 4096
-NCOLS = 8192
+SWEEP_KERNEL = "k_sweep_st"
 SEED = 3
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "hbm_traffic.json")
+
+# name -> (generator kind, m, ns, description)
+WORKLOADS = {
+    "cfg4": ("tall", 32768, 8192, "cfg4: 32768x8192 float64 tableau, G_tall seed 3"),
+    "cfg3": ("mixed", 4096, 4096, "cfg3: 4096x8192 float64 tableau, G_mixed seed 3"),
+}
 
 
 def pivot_bytes(m: int, n: int) -> int:
-    """Algorithmic bytes of one pivot: read+write the whole
-    tableau, the row-0 scan and the column+b ratio gather."""
+    """Algorithmic bytes of one unblocked pivot: read+write
+    the whole tableau, the row-0 scan and the column+b ratio gather."""
     return 8 * (2 * (m + 1) * (n + 1) + (n + 1) + 2 * (m + 1))
 
 
-SWEEP_KERNEL = "k_sweep_st"
-
-
 def sweep_bytes(rows: int, n: int, block: int) -> int:
-    """Algorithmic bytes of one sweep (k_sweep_st) launch on `rows` local rows applying
-    `block` deferred pivots: read and write every row once, read the block's
-    pivot rows P and multiplier columns M."""
+    """Algorithmic bytes of one sweep (k_sweep_st) launch on `rows` local rows
+    applying `block` deferred pivots: read and write every row once, read the
+    group's pivot rows P and multiplier columns M once."""
     return 8 * (2 * rows * (n + 1) + block * (n + 1) + block * rows)
 
 
-def workload(nranks: int, rank: int):
-    """(kind, m, ns, n, row block) of this rank."""
-    if nranks == 1:
-        kind, m, ns = "mixed", ROWS_PER_GPU, NCOLS - ROWS_PER_GPU
-    else:
-        kind, m, ns = "tall", ROWS_PER_GPU * nranks, NCOLS
+def workload(name: str, nranks: int, rank: int):
+    """(kind, m, ns, n, first row, end row) of this rank's row block: the
+    engine's split (lp_create_sharded) -- contiguous blocks, m * r // N."""
+    kind, m, ns, _ = WORKLOADS[name]
     _, n = gen.shape(kind, m, ns)
-    rb = m * rank // nranks
-    re_ = m * (rank + 1) // nranks
-    return kind, m, ns, n, rb, re_
+    return kind, m, ns, n, m * rank // nranks, m * (rank + 1) // nranks
 
 
-def cpu_baseline(seconds_target: float = 15.0) -> dict:
-    """Exact-Fraction oracle (the reference's algorithm, oracle/exact.py) on
-    the first standard-rule pivot of cfg3, applied to a bounded row sample and
-    scaled to the full 4097-row tableau.  Single core."""
+def lib_digest() -> str:
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_traffic(path: str | None, block: int, workload_name: str, digest: str):
+    """HBM bytes per sweep launch measured by scripts/hbm_traffic.py (two
+    rocprofv3 --pmc passes of this bench), if measured on this very library
+    build (sha256 stamp), workload and pivots per sweep; else None."""
+    if path and os.path.exists(path):
+        with open(path) as f:
+            d = json.load(f)
+        for e in d.get("entries", [d]):
+            if (e.get("block") == block and e.get("workload") == workload_name
+                    and e.get("lib_sha256") == digest
+                    and e.get("kernel", "").split("<")[0] == SWEEP_KERNEL):
+                return e.get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline(name: str, seconds_target: float = 15.0) -> dict:
+    """The reference's algorithm on one host core: oracle/exact.py's
+    Fraction restatement of Tableau.pivot in the reference's own order of
+    operations (rowDiv, rowAddToObj, then rowSub over EVERY column of every
+    other row, tableau.py:254-308), on the first standard-rule pivot of the
+    workload, applied to a bounded sample of rows and scaled to all rows."""
     from oracle import exact
-    kind, m, ns = "mixed", ROWS_PER_GPU, NCOLS - ROWS_PER_GPU
-    T = gen.tableau(kind, m, ns, SEED)
-    # selection on the full tableau (cheap: row 0 + one column)
-    c = int(np.argmin(T[0, 1:]))
-    col = T[1:, 1 + c]
+    kind, m, ns, _ = WORKLOADS[name]
+    T0 = gen.rows(kind, m, ns, SEED, 0, 1)
+    c = int(np.argmin(T0[0, 1:]))
+    # the leaving row from the whole column (cheap; numpy)
+    col = np.empty(m)
+    b = np.empty(m)
+    for a in range(0, m, 4096):
+        R = gen.rows(kind, m, ns, SEED, 1 + a, 1 + min(a + 4096, m))
+        col[a:a + len(R)] = R[:, 1 + c]
+        b[a:a + len(R)] = R[:, 0]
     with np.errstate(divide="ignore", invalid="ignore"):
-        q = np.where(col > 0, T[1:, 0] / np.where(col > 0, col, 1), np.inf)
+        q = np.where(col > 0, b / np.where(col > 0, col, 1), np.inf)
     r = int(np.argmin(q))
-    # sample: row 0, the pivot row and the first S other rows
+    prow = gen.rows(kind, m, ns, SEED, 1 + r, 2 + r)
+    total, rows_done, S, i0 = 0.0, 0, 16, 0
     t0 = time.perf_counter()
-    S, total, rows_done = 16, 0.0, 0
-    others = [i for i in range(m) if i != r]
-    while total < seconds_target and rows_done + S <= len(others):
-        pick = others[rows_done:rows_done + S]
-        sub = exact.from_array(np.vstack([T[:1], T[1 + r:2 + r], T[[1 + i for i in pick]]]))
+    while total < seconds_target and i0 + S <= m:
+        pick = [i for i in range(i0, i0 + S) if i != r]
+        blk = gen.rows(kind, m, ns, SEED, 1 + i0, 1 + i0 + S)
+        sub = exact.from_array(np.vstack([T0, prow, blk[[i - i0 for i in pick]]]))
         t1 = time.perf_counter()
-        exact.pivot(sub, 0, c)
+        exact.pivot_dense(sub, 0, c)
         total += time.perf_counter() - t1
-        rows_done += S
+        rows_done += len(pick)
+        i0 += S
         S = min(2 * S, 256)
         if time.perf_counter() - t0 > 3 * seconds_target:
             break
-    # rows_done updated rows (+ one row 0 and one pivot row per chunk, ignored:
-    # conservative) -> seconds for the m + 1 rows of a full pivot
-    sec_per_pivot = total / rows_done * (m + 1)
-    return {"value": 1.0 / sec_per_pivot, "unit": "pivots/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle/exact.py Fraction pivot #1 of cfg3 (G_mixed 4096x8192 seed 3) "
-                       f"on {rows_done} of 4097 rows ({total:.1f} s), scaled to all rows; "
-                       f"host has {os.cpu_count()} cores"),
-            "seconds_per_pivot": sec_per_pivot}
+    # the sample's other rows (+ row 0 and the pivot row per chunk, left out:
+    # conservative) -> seconds for the m + 1 rows of a whole pivot
+    sec = total / rows_done * (m + 1)
+    return {"value": 1.0 / sec, "unit": "pivots/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/exact.py pivot_dense (the reference's Fraction row operations, "
+                       f"every column) on pivot #1 of {name}, {rows_done} of {m + 1} rows "
+                       f"({total:.1f} s on one core), scaled to all rows; host has "
+                       f"{os.cpu_count()} cores"),
+            "seconds_per_pivot": sec}
 
 
 def config_table(cpu_budget: float = 20.0) -> None:
     """--configs: BASELINE.json's small configs on GPU 0, each next to the
     reference's algorithm on one host core (the exact-Fraction restatement,
-    oracle/exact.py: the cpu_baseline leg), one JSON line per config.  GPU
-    legs are whole calls (upload excluded), best of 3; CPU legs run to the end
-    or for cpu_budget seconds (then per pivot)."""
+    oracle/exact.py), one JSON line per config.  GPU legs are whole calls
+    (upload excluded), best of 3; CPU legs run to the end or for cpu_budget
+    seconds (then per pivot)."""
     from oracle import exact
 
     def gpu(T, job):
@@ -148,7 +179,7 @@ def config_table(cpu_budget: float = 20.0) -> None:
             p = exact.find_standard(F)
             if isinstance(p, str):
                 break
-            exact.pivot(F, *p)
+            exact.pivot_dense(F, *p)
             done += 1
         return time.perf_counter() - t0, done, False
 
@@ -168,44 +199,104 @@ def config_table(cpu_budget: float = 20.0) -> None:
             "gpu_pivots_per_s": ng / tg,
             "cpu_s": tc, "cpu_pivots": nc, "cpu_whole_run": whole,
             "cpu_pivots_per_s": nc / tc if tc > 0 else None,
-            "cpu_kind": "port: oracle/exact.py (Fraction), 1 core",
+            "cpu_kind": "port: oracle/exact.py (Fraction, the reference's row operations), 1 core",
         }), flush=True)
 
 
-def load_traffic(path: str | None, block: int):
-    """HBM bytes per sweep launch measured by scripts/hbm_traffic.py (two
-    rocprofv3 --pmc passes on this workload), or None if not measured for
-    this kernel and pivots-per-sweep setting."""
-    if path and os.path.exists(path):
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("block") == block and d.get("kernel", "").split("<")[0] == SWEEP_KERNEL:
-            return d.get("hbm_bytes_per_launch")
-    return None
+def upload(engines, kind, m, ns, spans, blk=2048):
+    """rows of the workload into each engine (row 0 + its row block)"""
+    for e, (a0, a1) in zip(engines, spans):
+        e.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
+        for a in range(a0, a1, blk):
+            e.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + min(a + blk, a1)))
+
+
+def accounting(steps: int, block: int, elapsed: float, sweep_avg_ms: float, sel_avg_ms: float,
+               local_rows: int, n: int) -> dict:
+    """the per-launch figures of a timed run of `steps` groups of `block`
+    pivots: every sweep and selection launch carries exactly `block` pivots"""
+    pivots = steps * block
+    sweep_b = sweep_bytes(local_rows, n, block)
+    achieved = sweep_b / (sweep_avg_ms * 1e-3) / 1e9 if sweep_avg_ms > 0 else 0.0
+    return {
+        "pivots": pivots,
+        "pivots_per_s": pivots / elapsed,
+        "ms_per_step": 1e3 * elapsed / steps,
+        "sweep_bytes_per_launch": sweep_b,
+        "achieved_GBps": achieved,
+        "sweep_time_share": sweep_avg_ms * steps / (elapsed * 1e3),
+        "selection_us_per_pivot": 1e3 * sel_avg_ms / block if sel_avg_ms > 0 else None,
+        "selection_time_share": sel_avg_ms * steps / (elapsed * 1e3) if sel_avg_ms > 0 else None,
+    }
+
+
+def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int):
+    """warmup groups, then exactly `steps` timed groups bracketed by the
+    barrier + stream sync (lp_run ends with a stream sync)."""
+    st, done = eng.run(_lib.RULE_STANDARD, warmup * block)
+    if done != warmup * block:
+        raise SystemExit(f"warmup ended early: status {st} after {done} pivots")
+    barrier()
+    if not os.environ.get("LPGPU_BENCH_NO_EVENTS"):
+        eng.profile(True, every=every)
+    t0 = time.perf_counter()
+    st, done = eng.run(_lib.RULE_STANDARD, steps * block)
+    t1 = time.perf_counter()
+    barrier()
+    if done != steps * block:
+        raise SystemExit(f"timed run ended early: status {st} after {done} pivots")
+    upd_ms, upd_n = eng.update_time()
+    sel_ms, sel_n = eng.select_time()
+    eng.profile(False)
+    return t1 - t0, upd_ms / max(upd_n, 1), (sel_ms / sel_n if sel_n else 0.0), upd_n, sel_n
+
+
+def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, device: int,
+                   shards: int = 0) -> dict:
+    """one workload on one GPU (or as `shards` in-process row shards of it,
+    a diagnostic): timing, roofline and selection figures"""
+    kind, m, ns, n, _, _ = workload(name, 1, 0)
+    if shards:
+        engs = _lib.create_group(m, n, shards, device=device)
+        spans = [(e.row_begin, e.row_begin + e.row_count) for e in engs]
+    else:
+        engs = [_lib.Engine(m, n, device=device)]
+        spans = [(0, m)]
+    for e in engs:
+        e.set_block(block)
+    upload(engs, kind, m, ns, spans)
+    elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(engs[0], steps, warmup, block, lambda: None, every)
+    path, fallbacks = engs[0].exchange_path()
+    acc = accounting(steps, block, elapsed, sw_ms, sel_ms, spans[0][1] - spans[0][0] + 1, n)
+    acc.update(path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks,
+               sweep_avg_us=sw_ms * 1e3, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
+               selection_avg_launch_us=sel_ms * 1e3)
+    for e in reversed(engs):
+        e.close()
+    return acc
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4096)
-    ap.add_argument("--warmup", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=128,
+                    help="timed steps; one step = one group of --block pivots + one sweep")
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--block", type=int, default=32,
                     help="pivots deferred into one sweep of the tableau (1 = eager)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg4")
+    ap.add_argument("--no-cfg3", action="store_true", help="N = 1: skip the cfg3 leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01",
-                                                            "hbm_traffic.json"))
-    ap.add_argument("--emulate-ranks", type=int, default=0,
-                    help="1-GPU diagnostic: run the N-rank job's whole tableau on one GPU")
+    ap.add_argument("--traffic-json", default=TRAFFIC_JSON)
     ap.add_argument("--exchange", choices=["auto", "peer", "rccl"], default="auto",
                     help="N > 1: device-side peer exchange per pivot (auto: if its setup "
                          "check passes on every rank) or one RCCL collective per pivot")
     ap.add_argument("--no-rccl", action="store_true",
-                    help="N > 1 without an RCCL communicator (peer exchange only; lets two "
-                         "ranks share one GPU for testing)")
+                    help="N > 1 without an RCCL communicator (peer exchange and the host "
+                         "all-gather; lets ranks share one GPU for testing)")
     ap.add_argument("--group-shards", type=int, default=0,
-                    help="1-GPU diagnostic: the N-rank row-sharded job as N in-process shards "
-                         "on one GPU (device copies instead of RCCL)")
+                    help="1-GPU diagnostic: the workload as S in-process row shards on one GPU")
     ap.add_argument("--profile-every", type=int, default=8,
                     help="time every k-th launch of each kernel with HIP events (1 = all)")
     ap.add_argument("--configs", action="store_true",
@@ -226,24 +317,29 @@ def main():
 
     ndev = _lib.device_count()
     device = local % ndev if ndev else local     # one rank per GPU; wraps only on smaller boxes
-    dist = None
-    if world > 1:
+    B = args.block
+    digest = lib_digest()
+    kind, m, ns, n, rb, re_ = workload(args.workload, world, rank)
+    out = {"metric": METRIC, "unit": "pivots/s"}
+
+    if world == 1:
+        leg = single_gpu_leg(args.workload, args.steps, args.warmup, B, args.profile_every, device,
+                             args.group_shards)
+        elapsed_pps, devices = leg["pivots_per_s"], 1
+        parallelism = (f"1 GPU ({leg['path']})" if not args.group_shards else
+                       f"diagnostic: {args.group_shards} in-process row shards on 1 GPU ({leg['path']})")
+        sweep_ms, local_rows = leg["sweep_avg_us"] * 1e-3, (m // (args.group_shards or 1)) + 1
+        acc = leg
+    else:
+        import torch
         import torch.distributed as dist  # plumbing only: uid exchange, barriers, max
         dist.init_process_group("gloo")
-
-    nsim = args.emulate_ranks or args.group_shards or world
-    kind, m, ns, n, rb, re_ = workload(nsim, rank if world > 1 else 0)
-    if world == 1:
-        rb, re_ = 0, m
-    shards = None
-    exchange = None
-    if world > 1:
-        import torch
         box = [None if args.no_rccl else (_lib.comm_unique_id() if rank == 0 else None)]
         dist.broadcast_object_list(box, src=0)
         eng = _lib.create_sharded(m, n, rank, world, box[0], device=device)
         assert (eng.row_begin, eng.row_count) == (rb, re_ - rb)
-        # device-side exchange between the ranks; every rank must agree on it
+        if args.no_rccl:
+            eng.set_host_allgather(_lib.gloo_allgather())
         ok, why = 0, "not requested"
         if args.exchange != "rccl" or args.no_rccl:
             try:
@@ -255,152 +351,105 @@ def main():
                 why = str(ex)
         flag = torch.tensor([ok], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag[0]) == 1:
-            exchange = "device peer stores over xGMI (one persistent selection launch per group)"
-        else:
-            if args.exchange == "peer" or args.no_rccl:
+        if int(flag[0]) != 1:
+            if args.exchange == "peer":
                 raise SystemExit(f"peer exchange unavailable on some rank: {why}")
             if ok:
                 eng.peer_enable(False)
-            exchange = "RCCL collectives per pivot" + (f" (peer setup failed: {why})" if why else "")
-    elif args.group_shards:
-        shards = _lib.create_group(m, n, args.group_shards, device=device)
-        eng = shards[0]
-        rb, re_ = eng.row_begin, eng.row_begin + eng.row_count
-    else:
-        eng = _lib.Engine(m, n, device=device)
-    eng.set_block(args.block)
-    blk = 2048
-    for e in (shards or [eng]):
-        e.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
-        a0, a1 = (e.row_begin, e.row_begin + e.row_count) if shards else (rb, re_)
-        for a in range(a0, a1, blk):
-            b = min(a + blk, a1)
-            e.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + b))
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def upload():
-        for e in (shards or [eng]):
-            e.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
-            a0, a1 = (e.row_begin, e.row_begin + e.row_count) if shards else (rb, re_)
-            for a in range(a0, a1, blk):
-                e.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + min(a + blk, a1)))
-
-    try:
-        st, done = eng.run(_lib.RULE_STANDARD, args.warmup)     # ends with a stream sync
-        warm_ok = 1
-    except _lib.DeviceError as ex:
-        if dist is None or exchange is None or not exchange.startswith("device"):
-            raise
-        warm_ok, why = 0, str(ex)
-    if dist is not None and exchange is not None and exchange.startswith("device"):
-        import torch
-        flag = torch.tensor([warm_ok], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag[0]) == 0:
-            # the peer exchange failed on some rank: every rank starts over on
-            # the RCCL per-pivot path (identical results)
-            if args.no_rccl:
-                raise SystemExit("peer exchange failed during warmup and there is no RCCL communicator")
-            eng.peer_enable(False)
-            exchange = "RCCL collectives per pivot (peer exchange failed in warmup)"
-            upload()
-            st, done = eng.run(_lib.RULE_STANDARD, args.warmup)
-    if done != args.warmup:
-        raise SystemExit(f"warmup ended early: status {st} after {done} pivots")
-    barrier()
-    # kernel durations: HIP events recorded by every PROFILE_EVERY-th launch of
-    # each kernel inside the timed run (events on every launch cost ~3 % of
-    # the rate; LPGPU_BENCH_NO_EVENTS=1 times the run with none)
-    if not os.environ.get("LPGPU_BENCH_NO_EVENTS"):
-        eng.profile(True, every=args.profile_every)
-    t0 = time.perf_counter()
-    st, done = eng.run(_lib.RULE_STANDARD, args.steps)      # enqueue + final stream sync
-    t1 = time.perf_counter()
-    barrier()
-    if done != args.steps:
-        raise SystemExit(f"timed run ended early: status {st} after {done} pivots")
-    upd_ms, upd_n = eng.update_time()
-    sel_ms, sel_n = eng.select_time()
-    eng.profile(False)
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed, upd_ms / max(upd_n, 1)], dtype=torch.float64)
+        eng.set_block(B)
+        upload([eng], kind, m, ns, [(rb, re_)])
+        elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(eng, args.steps, args.warmup, B,
+                                                        dist.barrier, args.profile_every)
+        t = torch.tensor([elapsed, sw_ms, sel_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, upd_avg_ms = float(t[0]), float(t[1])
-    else:
-        upd_avg_ms = upd_ms / max(upd_n, 1)
+        elapsed, sw_ms, sel_ms = float(t[0]), float(t[1]), float(t[2])
+        # distinct GPUs of the job (ranks wrap onto fewer GPUs on a small box)
+        ids = [None] * world
+        dist.all_gather_object(ids, (os.uname().nodename, device))
+        devices = len(set(ids))
+        path, fallbacks = eng.exchange_path()
+        share = "" if devices == world else f", {world} ranks sharing {devices} GPU(s)"
+        parallelism = (f"row-shard x{world} over {'xGMI' if devices == world else 'one GPU'}: "
+                       f"{_lib.PATH_NAMES.get(path, path)}{share}")
+        local_rows = (re_ - rb) + 1          # the largest block: ranks differ by <= 1 row
+        sweep_ms = sw_ms
+        acc = accounting(args.steps, B, elapsed, sw_ms, sel_ms, local_rows, n)
+        acc.update(fallbacks=fallbacks, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
+                   selection_avg_launch_us=sel_ms * 1e3)
+        elapsed_pps = acc["pivots_per_s"]
 
-    lp_pps = args.steps / elapsed
-    groups = -(-args.steps // args.block)          # sweeps (and selection launches) in the run
-    local_rows = (re_ - rb) + 1
-    sweep_b = sweep_bytes(local_rows, n, args.block)
-    achieved = sweep_b / (upd_avg_ms * 1e-3) / 1e9 if upd_avg_ms > 0 else 0.0
-    traffic = load_traffic(args.traffic_json, args.block) if world == 1 else None
-    out = {
-        "metric": METRIC,
-        "value": lp_pps * world,
-        "unit": "pivots/s",
-        "n_gpus": world,
+    desc = WORKLOADS[args.workload][3]
+    traffic = (load_traffic(args.traffic_json, B, args.workload, digest)
+               if world == 1 and not args.group_shards else None)
+    out.update({
+        "value": elapsed_pps,
+        "n_gpus": devices,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
+        "ms_per_step": acc["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (counter-based splitmix64 dyadic k/64 LP, lpsol_amd.generators)",
         "config": {
-            "workload": ("cfg3: 4096x8192 float64 tableau, G_mixed seed 3" if nsim == 1 else
-                         f"G_tall {m}x{n} float64 tableau seed 3, {ROWS_PER_GPU} rows per GPU"
-                         + (" (cfg4)" if nsim == 8 else "")
-                         + (f" [diagnostic: whole tableau on 1 GPU]" if args.emulate_ranks else "")
-                         + (f" [diagnostic: {nsim} in-process shards on 1 GPU]" if args.group_shards else "")),
-            "m": m, "n": n, "rows_per_gpu": re_ - rb, "rule": "standard (findPivotStandard)",
-            "parallelism": f"row-shard x{world}" + (f": {exchange}" if world > 1 else ""),
+            "workload": desc, "m": m, "n": n, "rows_per_gpu": re_ - rb if world > 1 else m,
+            "rule": "standard (findPivotStandard)",
+            "step": f"{B} pivots selected + one elimination sweep of the tableau",
+            "parallelism": parallelism,
         },
-        "lp_pivots_per_s": lp_pps,
-        "pivots_per_sweep": args.block,
+        "pivots_per_step": B,
+        "pivots_timed": acc["pivots"],
+        "us_per_pivot": 1e6 / elapsed_pps,
         # SURVEY §8(d) bytes of one unblocked pivot x pivots/s: the bandwidth an
-        # immediate-update engine would need for this rate (exceeds HBM peak
-        # once pivots are deferred -- that is the point of the sweep)
-        "unblocked_equivalent_GBps": pivot_bytes(m, n) * lp_pps / 1e9,
+        # immediate-update engine would need for this rate
+        "unblocked_equivalent_GBps": pivot_bytes(m, n) * elapsed_pps / 1e9,
         "roofline": {
-            "kernel": f"{SWEEP_KERNEL} (rank-{args.block} elimination, {args.block} deferred pivots)",
+            "kernel": f"{SWEEP_KERNEL} (rank-{B} elimination of {local_rows} local rows)",
             "bound": "hbm",
-            "achieved": achieved,
+            "achieved": acc["achieved_GBps"],
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS,
+            "frac": acc["achieved_GBps"] / HBM_PEAK_GBPS,
             "traffic": traffic,
-            "bytes_per_launch": sweep_b,
-            "avg_launch_us": upd_avg_ms * 1e3,
-            "time_share": upd_avg_ms * groups / (elapsed * 1e3),
-            "launches_timed": upd_n,
+            "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch, measured on this library "
+                             "build (profiles/r02/hbm_traffic.json)" if traffic else
+                             "not measured on this library build / workload"),
+            "bytes_per_launch": acc["sweep_bytes_per_launch"],
+            "avg_launch_us": sweep_ms * 1e3,
+            "time_share": acc["sweep_time_share"],
         },
-    }
-    if sel_n:
-        # the other kernel of the path: one persistent launch selects a group of
-        # pivots; its time is the chain of per-pivot summary exchanges and
-        # dependent loads (latency), not bytes
-        out["selection"] = {
+        "selection": {
             "kernel": "k_group (persistent pivot selection, latency-bound)",
-            "avg_launch_us": 1e3 * sel_ms / sel_n,
-            "pivots_per_launch": args.block,
-            "us_per_pivot": 1e3 * sel_ms / sel_n / args.block,
-            "time_share": sel_ms / max(sel_n, 1) * groups / (elapsed * 1e3),
-            "launches_timed": sel_n,
+            "us_per_pivot": acc["selection_us_per_pivot"],
+            "avg_launch_us": acc["selection_avg_launch_us"],
+            "pivots_per_launch": B,
+            "time_share": acc["selection_time_share"],
+        },
+        "fallbacks": acc["fallbacks"],
+        "lib_sha256": digest,
+    })
+    if world == 1 and args.workload != "cfg3" and not args.no_cfg3 and not args.group_shards:
+        c3 = single_gpu_leg("cfg3", args.steps, args.warmup, B, args.profile_every, device)
+        out["cfg3"] = {
+            "workload": WORKLOADS["cfg3"][3], "value": c3["pivots_per_s"], "unit": "pivots/s",
+            "ms_per_step": c3["ms_per_step"], "us_per_pivot": 1e6 / c3["pivots_per_s"],
+            "roofline": {"kernel": f"{SWEEP_KERNEL} (rank-{B} elimination of 4097 rows)", "bound": "hbm",
+                         "achieved": c3["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": c3["achieved_GBps"] / HBM_PEAK_GBPS,
+                         "traffic": load_traffic(args.traffic_json, B, "cfg3", digest),
+                         "bytes_per_launch": c3["sweep_bytes_per_launch"],
+                         "avg_launch_us": c3["sweep_avg_us"], "time_share": c3["sweep_time_share"]},
+            "selection": {"us_per_pivot": c3["selection_us_per_pivot"],
+                          "time_share": c3["selection_time_share"]},
+            "path": c3["path"], "fallbacks": c3["fallbacks"],
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
-    if dist is not None:
+    if world > 1:
+        eng.close()
         dist.destroy_process_group()
 
 

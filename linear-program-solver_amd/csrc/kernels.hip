@@ -2171,9 +2171,13 @@ static const void *group_kernel(int nr, int ipl, int rpl, bool xr)
 
 // resident k_group blocks per CU the launch may rely on: the runtime's
 // occupancy answer for the compiled kernel (its VGPRs, SGPRs, static and
-// dynamic LDS), one less unless LDS is what limits it (MI355X_MICROARCH,
-// residency: the API can admit one block per CU more than the hardware does
-// at some SGPR counts; the LDS bound is exact)
+// dynamic LDS), capped by the LDS a CU holds when every block's share is
+// rounded up to 2 KB (allocation granule and slack: the runtime admitted 3
+// blocks of 53 KB per CU, of which the hardware did not keep the last ones
+// resident -- 8 in-process cfg4 shards timed out, round 2), one less unless
+// that LDS cap is what limits it
+// (MI355X_MICROARCH, residency: the API can admit one block per CU more than
+// the hardware does at some SGPR counts)
 static int group_per_cu(const void *fn, size_t lds)
 {
     int n = 0;
@@ -2185,8 +2189,10 @@ static int group_per_cu(const void *fn, size_t lds)
     size_t stat = 0;
     if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
     (void)hipGetLastError();
-    const long long lds_cap = (long long)(160 * 1024) / (long long)(lds + stat);
-    return n == lds_cap ? n : n - 1;
+    const long long per = ((long long)(lds + stat) + 2047) / 2048 * 2048;
+    const long long lds_cap = (long long)(160 * 1024) / per;
+    if (n >= lds_cap) return (int)lds_cap;
+    return n - 1;
 }
 
 static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int xr, int nshard, int share)
@@ -2201,49 +2207,68 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
         xcd_on = v ? std::atoi(v) : 1;
     }
     const int cus = sweep_cus(), xcd_cus = cus / 8;
-    for (int rpl = 1; rpl <= GROUP_MAXRPL; ++rpl) {
-        // at least one own row per lane-slot; every lane at most 4 columns
-        // (2 where a few extra blocks achieve it); more blocks where the LDS
-        // of one would exceed GROUP_LDS_MAX
-        long long g = (rc + 64LL * rpl - 1) / (64LL * rpl);
-        if (g < GROUP_MINBLOCKS) g = GROUP_MINBLOCKS;
-        const long long g2 = (ld + 2 * GROUP_THREADS - 1) / (2 * GROUP_THREADS);
-        const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
-        if (g2 > g && g2 <= g + g / 8) g = g2;
-        if (g4 > g) g = g4;
-        while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, bmax) > GROUP_LDS_MAX) g *= 2;
-        if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
-        const long long cpb = (ld + g - 1) / g, rpb = (rc + g - 1) / g;
-        const long long lds = group_lds(rc, ld, g, bmax);
-        if (cpb > 4 * GROUP_THREADS || rpb > (long long)rpl * GROUP_THREADS || lds > GROUP_LDS_MAX) continue;
-        int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
-        nr = nr <= 1 ? 1 : nr <= 2 ? 2 : 4;
-        int ipl = (int)((cpb + GROUP_THREADS - 1) / GROUP_THREADS);
-        ipl = ipl <= 2 ? 2 : (ipl == 3 && nr <= 2) ? 3 : 4;
-        if (rpl == 2) nr = 4;
-        const void *fn = group_kernel(nr, ipl, rpl, xr != 0);
-        if (!fn) continue;
-        const int per_cu = group_per_cu(fn, (size_t)lds);
-        if (per_cu < 1) continue;
-        G.nr = nr;
-        G.ipl = ipl;
-        G.rpl = rpl;
-        G.lds = (size_t)lds;
-        G.per_cu = per_cu;
-        // every block of every launch that waits on this one must be
-        // resident at the same time: one XCD (L2-resident hand-offs) when
-        // they fit there, else the whole device
-        if (xcd_on && xr != 1 && nshard == 1 && share == 1 && g <= (long long)per_cu * xcd_cus) {
+    // candidate block counts, preferred first: at least one own row per
+    // lane-slot, every lane at most 4 columns; with a few extra blocks every
+    // lane down to 2 columns ("wide"), or not ("narrow", fewer blocks: fits
+    // where the wide one does not); more blocks where one's LDS would exceed
+    // GROUP_LDS_MAX
+    struct Cand {
+        long long g;
+        int rpl;
+    };
+    Cand cand[2 * GROUP_MAXRPL];
+    int nc = 0;
+    for (int rpl = 1; rpl <= GROUP_MAXRPL; ++rpl)
+        for (int wide = 1; wide >= 0; --wide) {
+            long long g = (rc + 64LL * rpl - 1) / (64LL * rpl);
+            if (g < GROUP_MINBLOCKS) g = GROUP_MINBLOCKS;
+            const long long g2 = (ld + 2 * GROUP_THREADS - 1) / (2 * GROUP_THREADS);
+            const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
+            if (wide && g2 > g && g2 <= g + g / 8) g = g2;
+            if (g4 > g) g = g4;
+            while (g < GROUP_MAXBLOCKS && group_lds(rc, ld, g, bmax) > GROUP_LDS_MAX) g *= 2;
+            if (g > GROUP_MAXBLOCKS) g = GROUP_MAXBLOCKS;
+            bool dup = false;
+            for (int k = 0; k < nc; ++k) dup = dup || (cand[k].g == g && cand[k].rpl == rpl);
+            if (!dup) cand[nc++] = Cand{g, rpl};
+        }
+    // every block of every launch that waits on this one must be resident at
+    // the same time.  Workgroups are dealt round-robin over the 8 XCDs, so
+    // each XCD must hold its eighth: one XCD (L2-resident hand-offs, xmode)
+    // where the blocks fit there, else the whole device
+    for (int pass = 0; pass < 2; ++pass)
+        for (int k = 0; k < nc; ++k) {
+            const long long g = cand[k].g;
+            const int rpl = cand[k].rpl;
+            const long long cpb = (ld + g - 1) / g, rpb = (rc + g - 1) / g;
+            const long long lds = group_lds(rc, ld, g, bmax);
+            if (cpb > 4 * GROUP_THREADS || rpb > (long long)rpl * GROUP_THREADS || lds > GROUP_LDS_MAX)
+                continue;
+            int nr = (int)((g + GROUP_THREADS - 1) / GROUP_THREADS);
+            nr = nr <= 1 ? 1 : nr <= 2 ? 2 : 4;
+            int ipl = (int)((cpb + GROUP_THREADS - 1) / GROUP_THREADS);
+            ipl = ipl <= 2 ? 2 : (ipl == 3 && nr <= 2) ? 3 : 4;
+            if (rpl == 2) {
+                nr = 4;
+                ipl = ipl <= 2 ? 2 : 4;
+            }
+            const void *fn = group_kernel(nr, ipl, rpl, xr != 0);
+            if (!fn) continue;
+            const int per_cu = group_per_cu(fn, (size_t)lds);
+            if (per_cu < 1) continue;
+            const bool one = pass == 0;
+            if (one && !(xcd_on && xr != 1 && nshard == 1 && share == 1 && g <= (long long)per_cu * xcd_cus))
+                continue;
+            if (!one && (g * nshard * share + 7) / 8 > (long long)per_cu * xcd_cus) continue;
             G.g = g;
-            G.xmode = 1;
+            G.nr = nr;
+            G.ipl = ipl;
+            G.rpl = rpl;
+            G.lds = (size_t)lds;
+            G.per_cu = per_cu;
+            G.xmode = one ? 1 : 0;
             return G;
         }
-        if (g * nshard * share <= (long long)per_cu * cus) {
-            G.g = g;
-            G.xmode = 0;
-            return G;
-        }
-    }
     return GroupGeom{};
 }
 

@@ -51,6 +51,7 @@ struct lp_handle {
     unsigned spin_max = 1u << 22;   // polls of one k_group exchange before it gives up
     unsigned xwait_ms = 30000;      // bound of a cross-rank wait (XR)
     int fault_launch = 0, fault_t = 0;   // tests: LPGPU_FAULT=<launch>:<pivot>
+    bool strict = false;            // LPGPU_STRICT=1 (tests): a timed-out group is an error
     // row-sharded persistent selection: device-side exchange between ranks
     unsigned long long *xbuf = nullptr;     // this rank's exchange buffer (peers write it)
     unsigned long long **dpeer = nullptr;   // device table: every rank's buffer
@@ -339,6 +340,7 @@ static int alloc_handle(lp_handle *h)
     if (const char *v = std::getenv("LPGPU_SPIN_MAX")) h->spin_max = (unsigned)std::strtoul(v, nullptr, 10);
     if (const char *v = std::getenv("LPGPU_XWAIT_MS")) h->xwait_ms = (unsigned)std::strtoul(v, nullptr, 10);
     if (const char *v = std::getenv("LPGPU_FAULT")) std::sscanf(v, "%d:%d", &h->fault_launch, &h->fault_t);
+    if (const char *v = std::getenv("LPGPU_STRICT")) h->strict = v[0] == '1';
     if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
@@ -1117,6 +1119,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         for (lp_handle *x : M) timed_out = timed_out || x->hctl->bar_timeout != 0;
         if (timed_out) {
             if (geo.g == 0) return fail(h, LP_DEVICE_ERROR, "exchange timed out on the per-pivot path");
+            if (h->strict) return fail(h, LP_DEVICE_ERROR, "persistent selection group timed out (LPGPU_STRICT)");
             CALL(recover_timeout(M, A, mode, rule, cap, first_seq));
             geo = lpk::GroupGeom{};
             for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));

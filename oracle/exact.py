@@ -90,6 +90,35 @@ def pivot(T, r: int, c: int) -> None:
             row[k] = row[k] - f * prow[k]
 
 
+def pivot_dense(T, r: int, c: int) -> None:
+    """``Tableau.pivot`` in the reference's own order of operations and with
+    its full row walks (``tableau.py:254-308``): ``rowDiv`` multiplies the
+    pivot row by 1/a (skipped when that is one, :257), ``rowAddToObj(r,
+    -c_c)`` and ``rowSub(rr, r, a_rr,c)`` for every other row (each skipped
+    when its multiplier is zero, :272,:285) add m * source[j] to EVERY entry
+    j of the destination row, zeros included.  Same result as ``pivot``;
+    this is the cost model of the reference's CPU path (bench.py's
+    cpu_baseline)."""
+    R, C = r + 1, c + 1
+    a = T[R][C]
+    if a == ZERO:
+        raise ZeroDivisionError(f"zero pivot {r},{c}")
+    inv = ONE / a
+    if inv != ONE:
+        T[R] = [x * inv for x in T[R]]
+    prow = T[R]
+    width = len(prow)
+    for rr in range(len(T)):
+        if rr == R:
+            continue
+        row = T[rr]
+        mult = -row[C]
+        if mult == ZERO:
+            continue
+        for k in range(width):
+            row[k] += mult * prow[k]
+
+
 # --------------------------------------------------------------------------
 # pivot selection  (lpsol/simplex.py:218-284)
 # --------------------------------------------------------------------------

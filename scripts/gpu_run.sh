@@ -19,7 +19,7 @@ for step in "$@"; do
     case "$step" in
         pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         drv) run bench_drv 300 python bench.py --steps 20 --warmup 5 ;;
-        cfg4) run bench_cfg4 600 python bench.py --no-cpu-baseline --emulate-ranks 8 --steps 256 ;;
+        benchd) run bench_default 600 python bench.py ;;
         pytestx) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
@@ -202,12 +202,15 @@ for step in "$@"; do
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_tall1_e*.log ;;
         pmc)
+            # HBM traffic of the sweep, per workload: two --pmc passes each
+            # (FETCH_SIZE and WRITE_SIZE do not fit one pass), one workload a run
             export TMPDIR=/tmp
-            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
-            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 "$PWD/bench.py" --steps 128 --warmup 16 --no-cpu-baseline
-            run pmc_json 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/hbm_traffic.json" --block 32 --kernel k_sweep_st
-            # later steps of this call (bench) report it as roofline.traffic
-            if [ -f "$OUT/hbm_traffic.json" ]; then cp "$OUT/hbm_traffic.json" profiles/r01/hbm_traffic.json; fi ;;
+            for W in ${PMC_WORKLOADS:-cfg4 cfg3}; do
+                run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
+                run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
+                run pmc_json_$W 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch_$W" "$OUT/pmc_write_$W" profiles/r02/hbm_traffic.json --block 32 --kernel k_sweep_st --workload $W
+            done
+            cp profiles/r02/hbm_traffic.json "$OUT/hbm_traffic.json" ;;
         proffinal)
             export TMPDIR=/tmp
             run rocprof_final 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_final" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline ;;

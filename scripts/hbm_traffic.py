@@ -5,7 +5,10 @@ scripts/gpu_run.sh runs bench.py twice under rocprofv3, once per counter.
 Both counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
 wide coalesced streaming read, so it is doubled (MI355X_MICROARCH.md §HBM).
 
-usage: python scripts/hbm_traffic.py FETCH_DIR WRITE_DIR OUT_JSON --block B
+usage: python scripts/hbm_traffic.py FETCH_DIR WRITE_DIR OUT_JSON --block B --workload W
+
+The result is stamped with the sha256 of the library build that ran (bench.py
+reports it as roofline.traffic only for that build, workload and block).
 """
 import argparse
 import csv
@@ -43,6 +46,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--block", type=int, default=16)
     ap.add_argument("--kernel", default="k_sweep_st")
+    ap.add_argument("--workload", default="cfg4")
     a = ap.parse_args()
     import bench
     fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
@@ -51,10 +55,13 @@ def main():
         raise SystemExit(f"no {a.kernel} dispatches with counters")
     f_kib, w_kib = statistics.mean(fetch), statistics.mean(write)
     hbm = (2.0 * f_kib + w_kib) * 1024.0
-    alg = bench.sweep_bytes(bench.ROWS_PER_GPU + 1, bench.NCOLS, a.block)
+    _, m, _, n, _, _ = bench.workload(a.workload, 1, 0)
+    alg = bench.sweep_bytes(m + 1, n, a.block)
     out = {
         "kernel": f"{a.kernel}<{a.block}>",
-        "workload": "cfg3 4096x8192 G_mixed seed 3 (bench.py, 1 GPU)",
+        "workload": a.workload,
+        "workload_desc": bench.WORKLOADS[a.workload][3] + " (bench.py, 1 GPU)",
+        "lib_sha256": bench.lib_digest(),
         "block": a.block,
         "dispatches": [len(fetch), len(write)],
         "FETCH_SIZE_KiB_mean": f_kib,
@@ -64,8 +71,15 @@ def main():
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": hbm / alg,
     }
+    # one entry per (workload, block, build): the file accumulates them
+    entries = []
+    if os.path.exists(a.out):
+        with open(a.out) as fh:
+            entries = json.load(fh).get("entries", [])
+    entries = [e for e in entries if (e.get("workload"), e.get("block"), e.get("lib_sha256")) !=
+               (out["workload"], out["block"], out["lib_sha256"])] + [out]
     with open(a.out, "w") as fh:
-        json.dump(out, fh, indent=1)
+        json.dump({"entries": entries}, fh, indent=1)
     print(json.dumps(out))
 
 

@@ -49,6 +49,15 @@ def fixture_exact(fx):
     return exact.from_array(fixture_input(fx))
 
 
+@pytest.fixture(autouse=True)
+def strict_engine(monkeypatch):
+    """every engine a test creates treats a timed-out persistent selection
+    group as an error (lpgpu.cpp, LPGPU_STRICT): the silent recovery onto
+    the per-pivot kernels would keep the results right and hide a
+    co-residency bug; the fault-injection tests switch it off"""
+    monkeypatch.setenv("LPGPU_STRICT", "1")
+
+
 @pytest.fixture(scope="session")
 def small_golden():
     return load_golden("small.json")

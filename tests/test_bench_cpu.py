@@ -1,20 +1,22 @@
 """bench.py's accounting, checked without a GPU: the algorithmic byte counts
-behind `roofline.achieved`, the weak-scaling row split, and
-the HBM traffic file it reports as `roofline.traffic`."""
+behind `roofline.achieved`, the strong-scaling row split,
+the per-launch figures of a timed run, the traffic file's stamp and the
+dense CPU baseline's pivot."""
 import json
-import os
 
+import numpy as np
 import pytest
 
-from conftest import ROOT
-
 import bench
+from lpsol_amd import generators as gen
+from oracle import exact
 
 
 def test_pivot_bytes_matches_survey():
     # B = 8 * [2 (m+1)(n+1) + (n+1) + 2 (m+1)]; cfg3: 537,198,632 B
     assert bench.pivot_bytes(4096, 8192) == 537_198_632
     assert bench.pivot_bytes(512, 1024) == 8_429_608
+    assert bench.pivot_bytes(32768, 8192) == 4_296_212_520
 
 
 def test_sweep_bytes_cfg3():
@@ -24,23 +26,66 @@ def test_sweep_bytes_cfg3():
     assert bench.sweep_bytes(rows, n, 32) == 540_213_776
 
 
+@pytest.mark.parametrize("name", ["cfg4", "cfg3"])
 @pytest.mark.parametrize("nranks", [1, 2, 4, 8])
-def test_workload_rows_partition(nranks):
-    spans = [bench.workload(nranks, r) for r in range(nranks)]
+def test_strong_scaling_rows_partition(name, nranks):
+    """the same tableau at every N, rows split like lp_create_sharded"""
+    spans = [bench.workload(name, nranks, r) for r in range(nranks)]
     kind, m, ns, n, _, _ = spans[0]
-    assert m == bench.ROWS_PER_GPU * nranks
-    assert n == 8192
+    assert (m, n) == ((32768, 8192) if name == "cfg4" else (4096, 8192))
     assert [s[4] for s in spans] == [m * r // nranks for r in range(nranks)]
-    assert spans[-1][5] == m
+    assert spans[0][4] == 0 and spans[-1][5] == m
     for a, b in zip(spans, spans[1:]):
         assert a[5] == b[4]                                  # contiguous, no overlap
 
 
-def test_traffic_file_is_for_this_workload():
-    path = os.path.join(ROOT, "profiles", "r01", "hbm_traffic.json")
-    d = json.load(open(path))
-    assert d["kernel"].startswith(bench.SWEEP_KERNEL)
-    assert d["algorithmic_bytes_per_launch"] == bench.sweep_bytes(4097, 8192, d["block"])
-    assert bench.load_traffic(path, d["block"]) == d["hbm_bytes_per_launch"]
-    assert bench.load_traffic(path, d["block"] + 1) is None
-    assert 1.0 <= d["traffic_over_algorithmic"] < 1.2
+@pytest.mark.parametrize("steps,block", [(20, 32), (1, 32), (128, 16)])
+def test_accounting_per_launch(steps, block):
+    """every launch of a timed run carries exactly `block` pivots (one step =
+    one group), so per-launch bytes and per-pivot selection time follow"""
+    a = bench.accounting(steps, block, elapsed=0.5, sweep_avg_ms=0.1, sel_avg_ms=0.2,
+                         local_rows=4097, n=8192)
+    assert a["pivots"] == steps * block
+    assert a["pivots_per_s"] == pytest.approx(steps * block / 0.5)
+    assert a["ms_per_step"] == pytest.approx(500.0 / steps)
+    assert a["sweep_bytes_per_launch"] == bench.sweep_bytes(4097, 8192, block)
+    assert a["achieved_GBps"] == pytest.approx(bench.sweep_bytes(4097, 8192, block) / 1e-4 / 1e9)
+    assert a["selection_us_per_pivot"] == pytest.approx(200.0 / block)
+    assert a["sweep_time_share"] == pytest.approx(0.1 * steps / 500.0)
+
+
+def test_traffic_needs_this_build(tmp_path):
+    """roofline.traffic is reported only for the library build, workload and
+    block the PMC passes measured (scripts/hbm_traffic.py stamps them)"""
+    p = tmp_path / "t.json"
+    d = {"kernel": "k_sweep_st<32>", "block": 32, "workload": "cfg4", "lib_sha256": "abc",
+         "hbm_bytes_per_launch": 123.0}
+    p.write_text(json.dumps(d))
+    assert bench.load_traffic(str(p), 32, "cfg4", "abc") == 123.0
+    assert bench.load_traffic(str(p), 32, "cfg4", "abd") is None
+    assert bench.load_traffic(str(p), 32, "cfg3", "abc") is None
+    assert bench.load_traffic(str(p), 16, "cfg4", "abc") is None
+    p.write_text(json.dumps({"entries": [dict(d, workload="cfg3", hbm_bytes_per_launch=7.0), d]}))
+    assert bench.load_traffic(str(p), 32, "cfg4", "abc") == 123.0
+    assert bench.load_traffic(str(p), 32, "cfg3", "abc") == 7.0
+
+
+def test_dense_pivot_is_the_reference_pivot():
+    """pivot_dense (the CPU baseline's cost model: every column, as
+    tableau.py:269-276) gives the same exact tableau as the oracle's pivot"""
+    T = gen.tableau("mixed", 12, 10, 4)
+    a, b = exact.from_array(T), exact.from_array(T)
+    for _ in range(6):
+        p = exact.find_standard(a)
+        if isinstance(p, str):
+            break
+        exact.pivot(a, *p)
+        exact.pivot_dense(b, *p)
+        assert a == b
+
+
+def test_cpu_baseline_sample_runs():
+    """the bounded cpu_baseline leg on the cfg3 workload, a short sample"""
+    r = bench.cpu_baseline("cfg3", seconds_target=0.5)
+    assert r["cores"] == 1 and r["kind"] == "port" and r["value"] > 0
+    assert "pivot_dense" in r["sample"]

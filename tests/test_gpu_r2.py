@@ -98,6 +98,7 @@ def test_timeout_recovery_redoes_the_group(monkeypatch, launch, t, mode):
     kernels: pivot sequence, stall counters and tableau as without a fault"""
     monkeypatch.setenv("LPGPU_FAULT", f"{launch}:{t}")
     monkeypatch.setenv("LPGPU_SPIN_MAX", "20000")
+    monkeypatch.delenv("LPGPU_STRICT")
     if mode == "run":
         T = gen.tableau("mixed", 300, 200, 5)
     else:
@@ -130,6 +131,7 @@ def test_timeout_recovery_shard_group(monkeypatch):
     collective per pivot"""
     monkeypatch.setenv("LPGPU_FAULT", "2:3")
     monkeypatch.setenv("LPGPU_SPIN_MAX", "20000")
+    monkeypatch.delenv("LPGPU_STRICT")
     monkeypatch.setenv("LPGPU_XWAIT_MS", "200")
     T = gen.tableau("mixed", 400, 150, 8)
     grp = _lib.create_group(T.shape[0] - 1, T.shape[1] - 1, 3)
