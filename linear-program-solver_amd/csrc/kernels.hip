@@ -734,8 +734,14 @@ __global__ void __launch_bounds__(PROW_THREADS) k_prow(Args A, int t, int grp, i
 // Same float64 operations as k_ratio + k_prow; no host round trips.
 // ---------------------------------------------------------------------------
 
-// diagnostic: block 0 / lane 0 records the 100 MHz real-time clock at phase
-// points of pivot t (LPGPU_STAMPS=1 builds the buffer; nothing stored otherwise)
+// diagnostic build only (-DLPK_STAMPS, `make variant NAME=stamps
+// DEFS=-DLPK_STAMPS`, run with LPGPU_STAMPS=1): block 0 / lane 0 records the
+// 100 MHz real-time clock at phase points of pivot t.  Compiled out of the
+// product build: a stamp's store, even behind a runtime test, made the
+// compiler wait for every outstanding store (s_waitcnt vmcnt(0)) before its
+// registers were reused, in the middle of the pivot-row phase.
+#ifdef LPK_STAMPS
+constexpr bool STAMPS = true;
 __device__ __forceinline__ void stamp(const Args &A, unsigned b, int t, int k)
 {
     if (A.stamps && b == 0 && threadIdx.x == 0 && t < BMAX)
@@ -747,6 +753,11 @@ __device__ __forceinline__ void bstamp(const Args &A, unsigned b, int t, int k)
     if (A.stamps && threadIdx.x == 0 && t < BMAX)
         *gp(A.stamps + BMAX * 16 + (b * BMAX + t) * 2 + k) = (long long)__builtin_amdgcn_s_memrealtime();
 }
+#else
+constexpr bool STAMPS = false;
+__device__ __forceinline__ void stamp(const Args &, unsigned, int, int) {}
+__device__ __forceinline__ void bstamp(const Args &, unsigned, int, int) {}
+#endif
 
 typedef unsigned long long u64;
 constexpr int NRMAX = (GROUP_MAXBLOCKS + GROUP_THREADS - 1) / GROUP_THREADS;
@@ -1034,7 +1045,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
 #pragma unroll
         for (int k = 0; k < NRMAX; ++k)
             if (threadIdx.x + k * GROUP_THREADS < G) same = same && wx[k][0] == xcc;
-        fast = __all(same);
+        // wave-uniform in a scalar register: st_x branches on it without
+        // exec masking (a divergent-looking branch around each store made
+        // the compiler wait for the stores before the next one)
+        fast = __builtin_amdgcn_readfirstlane(__all(same) ? 1 : 0) != 0;
     }
     const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= RPL nth)
     const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
@@ -1425,7 +1439,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                         }
                     }
             }
-            if (A.stamps) {       // diagnostic: the chain's results exist
+            if (STAMPS && A.stamps) {   // diagnostic: the chain's results exist
                 asm volatile("" ::"v"(xv[0]), "v"(xv[IPL - 1]));
                 stamp(A, b, t, 12);
             }
@@ -1434,7 +1448,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 const long long j = jc0 + tid + k * nth;
                 pv_[k] = (j == C) ? 1.0 : xv[k] / av;
             }
-            if (A.stamps) {
+            if (STAMPS && A.stamps) {
                 asm volatile("" ::"v"(pv_[0]), "v"(pv_[IPL - 1]));
                 stamp(A, b, t, 13);
             }
@@ -1605,22 +1619,34 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         if (tid == 0) sR[t] = R;
         double vmin = INFINITY, v0 = 0.0;
         double vv[IPL];                   // new row 0 on own columns (INFINITY: not a variable column)
+        double vn[IPL];                   // new row 0 on own columns
+        // every LDS read and all arithmetic first, then the LDS writes, then
+        // the global stores: no register of a pending store is rewritten in
+        // between (the compiler would wait for the store to complete)
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) vn[k] = upd(0, -1, f0, pv_[k], l0[kc[k]]);
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             const long long j = jc0 + tid + k * nth;
             vv[k] = INFINITY;
+            if (j == 0) v0 = vn[k];
+            if (j < jc1 && j >= 1 && j <= A.n) {
+                vmin = fmin(vmin, vn[k]);
+                vv[k] = vn[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (jc0 + tid + k * nth < jc1) {
+                lP[kc[k] * cs + t] = pv_[k];
+                l0[kc[k]] = vn[k];
+            }
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            const long long j = jc0 + tid + k * nth;
             if (j < jc1) {
-                const double p = pv_[k];
-                lP[kc[k] * cs + t] = p;
-                st_x(&A.P[t * A.ld + j], p, fast);
-                const double v = upd(0, -1, f0, p, l0[kc[k]]);
-                l0[kc[k]] = v;
-                st_x(&A.row0[j], v, fast);
-                if (j == 0) v0 = v;
-                if (j >= 1 && j <= A.n) {
-                    vmin = fmin(vmin, v);
-                    vv[k] = v;
-                }
+                st_x(&A.P[t * A.ld + j], pv_[k], fast);
+                st_x(&A.row0[j], vn[k], fast);
             }
         }
         __syncthreads();
