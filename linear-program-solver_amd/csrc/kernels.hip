@@ -1879,7 +1879,7 @@ __device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)
 // LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt,
 // 16 sc1 = write-through)
 template <int W, int RW, int NB, int LA = 0, int SA = 0>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(NB <= 32 ? 6 : 2, 8)))
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >= 16 ? 4 : NB <= 32 ? 6 : 2, 8)))
 k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
            const double *__restrict__ M, const long long *__restrict__ dR,
            const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
@@ -2160,8 +2160,14 @@ static int sweep_cus()
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0, hipEvent_t e1)
 {
     constexpr int W = 8, RW = 4, SA = 16;
+    static int wide = -1;   // A/B: 16-wave workgroups past 32 pivots
+    if (wide < 0) {
+        const char *v = std::getenv("LPGPU_SWEEP_WIDE");
+        wide = v ? std::atoi(v) : 0;
+    }
     const long long ns = (A.ld + 127) / 128;
-    const int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
+    int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
+    if (wide && nd_max > 32) bpc = 1;
     long long nrun = (long long)sweep_cus() * bpc / ns;
     if (nrun < 1) nrun = 1;
     long long run = (A.rows + nrun - 1) / nrun;
@@ -2171,11 +2177,17 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
 #define SWEEP_ST_ONE(NBV)                                                                            \
     hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, 0, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, A.T, \
                           A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
-    if (nd_max <= 16) SWEEP_ST_ONE(16);
+#define SWEEP_ST_WIDE(NBV)                                                                           \
+    hipExtLaunchKernelGGL((k_sweep_st<16, RW, NBV, 0, SA>), grid, dim3(64 * 16), 0, s, e0, e1, 0, A.T, A.T, \
+                          A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
+    if (wide && nd_max > 48) SWEEP_ST_WIDE(64);
+    else if (wide && nd_max > 32) SWEEP_ST_WIDE(48);
+    else if (nd_max <= 16) SWEEP_ST_ONE(16);
     else if (nd_max <= 32) SWEEP_ST_ONE(32);
     else if (nd_max <= 48) SWEEP_ST_ONE(48);
     else SWEEP_ST_ONE(64);
 #undef SWEEP_ST_ONE
+#undef SWEEP_ST_WIDE
     return hipGetLastError();
 }
 

@@ -321,11 +321,41 @@ extern "C" int lp_device_count(int *count)
     return LP_PIVOTED;
 }
 
+// Row pitch of the tableau in doubles: a multiple of 64 (512 B: rows start
+// on a cache line, 16-byte accesses stay aligned) that holds n + 1 columns
+// and is not "aliased".  A pitch of p x 512 B where p x d lies within
+// 1.5 min(k, 3) of k x 128 (k x 64 KiB) for some d = 1..4 sends the
+// selection's column gather -- one element from each of 32768 rows -- to few
+// HBM channels, at about twice the time of its neighbours
+// (scripts/gather_probe.hip, profiles/r02/gather_pitch.json: 3.6 us against
+// 1.7 us at p = 127/129 and 4.1 / 3.8 at 254 / 258; 2.2-2.6 at 43, 64, 86,
+// 172).  cfg3 / cfg4 (n = 8192): p = 129 -> 130.  At most 16 steps up.
+static bool pitch_aliased(int64_t p)
+{
+    for (int64_t d = 1; d <= 4; ++d) {
+        const int64_t q = p * d, k = (q + 64) / 128;
+        if (k < 1) continue;
+        const int64_t dist = q > 128 * k ? q - 128 * k : 128 * k - q;
+        if (2 * dist <= 3 * std::min<int64_t>(k, 3)) return true;
+    }
+    return false;
+}
+
+static int64_t row_pitch(int64_t n)
+{
+    const int64_t p0 = (n + 1 + 63) / 64;
+    const char *raw = std::getenv("LPGPU_LD_RAW");   // A/B: the plain rounded pitch
+    if ((raw && raw[0] == '1') || p0 < 16) return p0 * 64;
+    for (int64_t p = p0; p < p0 + 16; ++p)
+        if (!pitch_aliased(p)) return p * 64;
+    return p0 * 64;
+}
+
 static void init_geometry(lp_handle *h, int64_t m, int64_t n, int rank, int nranks)
 {
     h->m = m;
     h->n = n;
-    h->ld = (n + 1 + 63) / 64 * 64;
+    h->ld = row_pitch(n);
     h->rank = rank;
     h->nranks = nranks;
     h->rb = m * rank / nranks;

@@ -8,12 +8,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
 from lpsol_amd import _lib, generators as gen  # noqa: E402
 
-T = gen.tableau("mixed", 4096, 4096, 3)
-e = _lib.Engine(4096, 8192)
-e.upload(T)
-e.set_block(16)
-e.run(0, 64)
-e.run(0, 16)
+# python scripts/diag_stamps.py [kind m ns block]  (default: cfg3, 16 pivots a group)
+kind, m, ns, blk = (sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])) \
+    if len(sys.argv) > 4 else ("mixed", 4096, 4096, 16)
+mm, n = gen.shape(kind, m, ns)
+e = _lib.Engine(mm, n)
+for a in range(0, mm + 1, 2048):
+    e.put_rows(a, gen.rows(kind, m, ns, 3, a, min(a + 2048, mm + 1)))
+e.set_block(blk)
+e.run(0, 4 * blk)
+e.run(0, blk)
+print("workload", kind, m, ns, "block", blk, "path", e.exchange_path())
 BMAX = 64                      # lpk::BMAX: stamp rows per group
 buf = (C.c_longlong * (BMAX * 16))()
 assert e.lib.lpdiag_stamps(e.h, buf) == 0
@@ -21,7 +26,8 @@ assert e.lib.lpdiag_stamps(e.h, buf) == 0
 names = ["enter", "col0", "rload", "rcomp", "rpub", "gathR", "leave",
          "pload", "pcomp", "esum", "epub", "tail"]
 rows = []
-for t in range(15):
+NT = min(blk, 32) - 1
+for t in range(NT):
     st = [buf[t * 16 + k] for k in range(len(names))] + [buf[(t + 1) * 16]]
     d = [(st[k + 1] - st[k]) * 10 / 1000 for k in range(len(names))]   # 100 MHz ticks -> us
     rows.append(d)
@@ -30,18 +36,17 @@ avg = [sum(r[k] for r in rows[1:]) / (len(rows) - 1) for k in range(len(names))]
 print("avg", " ".join(f"{n}={x:4.2f}" for n, x in zip(names, avg)), "sum", round(sum(avg), 2))
 # pcomp split by stamps 12 (chain done) and 13 (division done): chain / div / store+row0
 sub = [[(buf[t * 16 + 12] - buf[t * 16 + 8]) / 100, (buf[t * 16 + 13] - buf[t * 16 + 12]) / 100,
-        (buf[t * 16 + 9] - buf[t * 16 + 13]) / 100] for t in range(1, 15)]
+        (buf[t * 16 + 9] - buf[t * 16 + 13]) / 100] for t in range(1, NT)]
 print("pcomp split: chain=%.2f div=%.2f store=%.2f" % tuple(sum(x[i] for x in sub) / len(sub) for i in range(3)))
 
 # per-block publish times: spread across blocks and the last blocks
-G = 65
 bb = (C.c_longlong * (256 * BMAX * 2))()
 assert e.lib.lpdiag_bstamps(e.h, bb) == 0
 spread = [[], []]
 last = {}
-for t in range(1, 15):
+for t in range(1, NT):
     for k in (0, 1):
-        v = [bb[(b * BMAX + t) * 2 + k] for b in range(G)]
+        v = [bb[(b * BMAX + t) * 2 + k] for b in range(256)]
         v = [x for x in v if x]
         if not v:
             continue

@@ -214,6 +214,37 @@ for step in "$@"; do
         proffinal)
             export TMPDIR=/tmp
             run rocprof_final 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_final" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline ;;
+        exp1)
+            # cfg4 by pivots per sweep; phase stamps of cfg3 and cfg4
+            for B in ${EXP_BLOCKS:-32 48 64}; do
+                run bench_cfg4_b$B 300 python bench.py --no-cpu-baseline --no-cfg3 --block $B --steps 24 --warmup 4
+            done
+            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
+            LPGPU_LIB=$L run stamps_cfg3 300 python scripts/diag_stamps.py mixed 4096 4096 32
+            LPGPU_LIB=$L run stamps_cfg4 300 python scripts/diag_stamps.py tall 32768 8192 32
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_cfg4_b*.log ;;
+        exp2)
+            run gather_probe 120 ./scripts/gather_probe
+            LPGPU_SWEEP_WIDE=1 run pytest_wide 300 python -u -m pytest tests/test_gpu_parity.py -k "block_size or cfg3_full" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for B in 48 64; do
+                LPGPU_SWEEP_WIDE=1 run bench_cfg4_w_b$B 300 python bench.py --no-cpu-baseline --no-cfg3 --block $B --steps 24 --warmup 4
+            done
+            for B in 32 48 64; do
+                LPGPU_SWEEP_WIDE=1 run bench_cfg3_w_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --block $B --steps 64 --warmup 4
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_cfg*_w_b*.log ;;
+        exp3)
+            run pytest_gpu 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for B in 32 48; do
+                run bench_cfg4_p_b$B 300 python bench.py --no-cpu-baseline --no-cfg3 --block $B --steps 24 --warmup 4
+                LPGPU_LD_RAW=1 run bench_cfg4_raw_b$B 300 python bench.py --no-cpu-baseline --no-cfg3 --block $B --steps 24 --warmup 4
+                run bench_cfg3_p_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --block $B --steps 64 --warmup 4
+                LPGPU_LD_RAW=1 run bench_cfg3_raw_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --block $B --steps 64 --warmup 4
+            done
+            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
+            LPGPU_LIB=$L run stamps_cfg4_p 300 python scripts/diag_stamps.py tall 32768 8192 32
+            LPGPU_LIB=$L run stamps_cfg3_p 300 python scripts/diag_stamps.py mixed 4096 4096 32
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_cfg*_p_b*.log "$OUT"/bench_cfg*_raw_b*.log ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
