@@ -46,7 +46,7 @@ from lpsol_amd import generators as gen  # noqa: E402
 
 METRIC = "pivots/sec + achieved HBM GB/s on dense float64 tableau, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-SWEEP_KERNEL = "k_sweep_st"
+SWEEP_KERNEL = "k_sweep_dp"
 SEED = 3
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "hbm_traffic.json")
 
@@ -264,11 +264,12 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
         spans = [(0, m)]
     for e in engs:
         e.set_block(block)
+    block = engs[0].get_block()          # the auto choice (--block 0) resolved
     upload(engs, kind, m, ns, spans)
     elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(engs[0], steps, warmup, block, lambda: None, every)
     path, fallbacks = engs[0].exchange_path()
     acc = accounting(steps, block, elapsed, sw_ms, sel_ms, spans[0][1] - spans[0][0] + 1, n)
-    acc.update(path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks,
+    acc.update(block=block, path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks,
                sweep_avg_us=sw_ms * 1e3, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
                selection_avg_launch_us=sel_ms * 1e3)
     for e in reversed(engs):
@@ -282,8 +283,9 @@ def main():
     ap.add_argument("--steps", type=int, default=128,
                     help="timed steps; one step = one group of --block pivots + one sweep")
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--block", type=int, default=32,
-                    help="pivots deferred into one sweep of the tableau (1 = eager)")
+    ap.add_argument("--block", type=int, default=0,
+                    help="pivots deferred into one sweep of the tableau (1 = eager, 0 = the "
+                         "engine's auto choice)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg4")
     ap.add_argument("--no-cfg3", action="store_true", help="N = 1: skip the cfg3 leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -330,6 +332,7 @@ def main():
                        f"diagnostic: {args.group_shards} in-process row shards on 1 GPU ({leg['path']})")
         sweep_ms, local_rows = leg["sweep_avg_us"] * 1e-3, (m // (args.group_shards or 1)) + 1
         acc = leg
+        B = leg["block"]
     else:
         import torch
         import torch.distributed as dist  # plumbing only: uid exchange, barriers, max
@@ -357,6 +360,7 @@ def main():
             if ok:
                 eng.peer_enable(False)
         eng.set_block(B)
+        B = eng.get_block()
         upload([eng], kind, m, ns, [(rb, re_)])
         elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(eng, args.steps, args.warmup, B,
                                                         dist.barrier, args.profile_every)
@@ -430,14 +434,15 @@ def main():
         "lib_sha256": digest,
     })
     if world == 1 and args.workload != "cfg3" and not args.no_cfg3 and not args.group_shards:
-        c3 = single_gpu_leg("cfg3", args.steps, args.warmup, B, args.profile_every, device)
+        c3 = single_gpu_leg("cfg3", args.steps, args.warmup, args.block, args.profile_every, device)
         out["cfg3"] = {
             "workload": WORKLOADS["cfg3"][3], "value": c3["pivots_per_s"], "unit": "pivots/s",
             "ms_per_step": c3["ms_per_step"], "us_per_pivot": 1e6 / c3["pivots_per_s"],
-            "roofline": {"kernel": f"{SWEEP_KERNEL} (rank-{B} elimination of 4097 rows)", "bound": "hbm",
+            "pivots_per_step": c3["block"],
+            "roofline": {"kernel": f"{SWEEP_KERNEL} (rank-{c3['block']} elimination of 4097 rows)", "bound": "hbm",
                          "achieved": c3["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": c3["achieved_GBps"] / HBM_PEAK_GBPS,
-                         "traffic": load_traffic(args.traffic_json, B, "cfg3", digest),
+                         "traffic": load_traffic(args.traffic_json, c3["block"], "cfg3", digest),
                          "bytes_per_launch": c3["sweep_bytes_per_launch"],
                          "avg_launch_us": c3["sweep_avg_us"], "time_share": c3["sweep_time_share"]},
             "selection": {"us_per_pivot": c3["selection_us_per_pivot"],

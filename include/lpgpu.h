@@ -193,7 +193,9 @@ int lp_pivot_log(lp_handle *h, int64_t *rc, int64_t cap, int64_t *count);
 /* Objective value getZ() = -T[0][0] (tableau.py:82-84, simplex.py:175-179). */
 int lp_objective(lp_handle *h, double *z);
 
-/* Pivots deferred into one sweep of the tableau (1..64, default 32).  Each
+/* Pivots deferred into one sweep of the tableau (1..64; 0 = auto, the
+ * default: the deepest of 64 / 48 / 32 whose persistent selection still fits
+ * one XCD, else 64; lp_get_block reports the value in use).  Each
  * pivot's selection and pivot row use current values computed on the fly; the
  * rank-1 eliminations of `pivots_per_sweep` pivots are applied to the stored
  * tableau in one pass (the same float64 operations in the same order, so the

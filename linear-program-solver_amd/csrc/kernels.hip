@@ -1903,6 +1903,152 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
     sweep_strip<W, RW, NB, LA, SA>(sp, sm, sr, T, Tout, P, M, nd, ld, rows, strip, r0, r1);
 }
 
+// ---------------------------------------------------------------------------
+// K3': the sweep with the multipliers broadcast by DPP (k_sweep_dp).  Same
+//   tiling as k_sweep_st (a workgroup owns a 128-column strip of a run of
+//   rows, 2 columns per lane, 4-row batches per wave, the strip's slice of P
+//   staged in LDS once), but a batch's multipliers never pass through LDS:
+//   every lane loads them straight into registers, 16 values per register --
+//   value v = 4 s' + k (pivot 4 c + s', batch row k) of chunk c sits in lane
+//   v of each 16-lane row -- and the FMA reads the one it needs with a
+//   row_newbcast DPP operand:
+//       v_fmac_f64_dpp x, -m, p row_newbcast:v      (x <- fma(-m[v], p, x))
+//   so per pivot and lane the LDS serves one 16-byte read (P) for 8 FMAs,
+//   a third of k_sweep_st's LDS traffic, and no instruction is spent on the
+//   broadcast.  Same float64 operations in the same order as upd(): bit-
+//   identical to k_sweep_st and oracle/lp_f64.c.
+// ---------------------------------------------------------------------------
+
+// pivots 4c .. 4c + 3 of one batch (4 rows x 2 columns per lane): 32 FMAs
+// whose multiplier operand is lane (4 s' + k) of the lane's 16-lane row of m.
+// The s_nop covers the VALU-write -> DPP-read hazard should the compiler copy
+// m into place right before the block.
+__device__ __forceinline__ void dp_chunk4(double2 (&x)[4], double m, double2 p0, double2 p1, double2 p2,
+                                          double2 p3)
+{
+#define DPF(XR, PV, L) "v_fmac_f64_dpp " XR ", -%8, " PV " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
+#define DPP_PIVOT(L0, L1, L2, L3, PX, PY)                                                     \
+    DPF("%0", PX, L0) DPF("%1", PY, L0) DPF("%2", PX, L1) DPF("%3", PY, L1) DPF("%4", PX, L2) \
+    DPF("%5", PY, L2) DPF("%6", PX, L3) DPF("%7", PY, L3)
+    asm volatile("s_nop 1\n" DPP_PIVOT(0, 1, 2, 3, "%9", "%10") DPP_PIVOT(4, 5, 6, 7, "%11", "%12")
+                     DPP_PIVOT(8, 9, 10, 11, "%13", "%14") DPP_PIVOT(12, 13, 14, 15, "%15", "%16")
+                 : "+v"(x[0].x), "+v"(x[0].y), "+v"(x[1].x), "+v"(x[1].y), "+v"(x[2].x), "+v"(x[2].y),
+                   "+v"(x[3].x), "+v"(x[3].y)
+                 : "v"(m), "v"(p0.x), "v"(p0.y), "v"(p1.x), "v"(p1.y), "v"(p2.x), "v"(p2.y), "v"(p3.x),
+                   "v"(p3.y));
+#undef DPP_PIVOT
+#undef DPF
+}
+
+template <int W, int NB, int SA, int PD>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PD >= 2 ? 3 : 4, 8)))
+k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
+           const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
+           int nstrips, long long run)
+{
+    constexpr int RW = 4;                        // rows per batch (4 x 4 = 16 values a register)
+    constexpr int NM = NB / 4;                   // multiplier registers (4 pivots each)
+    static_assert(NB % 4 == 0 && NB <= BMAX, "k_sweep_dp: pivots per sweep");
+    __shared__ double2 sp[NB][64];               // the strip's slice of P
+    __shared__ long long sr[NB];
+    const int nd = (int)ctl->ndef[grp];          // <= NB (the host's bound)
+    if (nd == 0 || ctl->bar_timeout) return;     // nothing deferred / group redone by the host
+    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
+    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
+    const long long r1 = min(rows, r0 + run);
+    if (r0 >= r1) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long c0 = (long long)strip * 128;
+    const int lo = min(lane * 2, (int)(ld - c0) - 2);
+    const int lob = lo * 8;
+    const int ldb = (int)(ld * 8);
+    const double *Ts = T + c0;
+    double *Tos = Tout + c0;
+    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
+    for (int s = wave; s < NB; s += W)
+        sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
+    // this lane's multiplier slot of register c: pivot 4 c + q / 4, row q % 4
+    // (q = lane % 16); pivots past nd read pivot nd - 1's (finite; their P is 0)
+    const int q = lane & 15, qs = q >> 2, qk = q & 3;
+    const int nch = (nd + 3) >> 2;               // chunks holding live pivots
+    // the multipliers of chunk c of the batch at rb (one register)
+    auto load_m = [&](long long rb, int c) {
+        const int mk = min(qk, (int)(r1 - 1 - rb));
+        const int sv = min(4 * c + qs, nd - 1);
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(buf_rsrc(M + rb), (sv * (int)rows + mk) * 8, 0, 0));
+    };
+    auto load_x = [&](double2 (&x)[RW], long long rb) {
+        const int kmax = (int)(r1 - 1 - rb);
+        const __amdgpu_buffer_rsrc_t rt = buf_rsrc(Ts + rb * ld);
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rt, lob, min(k, kmax) * ldb, 0));
+    };
+    const long long step = (long long)W * RW;
+    long long rb = r0 + (long long)wave * RW;
+    // PD batches of rows in flight ahead of the one being updated
+    double2 xn[RW], xnn[RW];
+    double m[NM];                                // the current batch's multipliers
+    if (rb < r1) {
+        load_x(xn, rb);
+#pragma unroll
+        for (int c = 0; c < NM; ++c) m[c] = load_m(rb, c);
+        if (PD >= 2 && rb + step < r1) load_x(xnn, rb + step);
+    }
+    __syncthreads();                             // sp, sr staged
+    for (; rb < r1; rb += step) {
+        double2 x[RW];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) x[k] = xn[k];
+        const long long rn = rb + step;
+        const bool more = rn < r1;
+        if (PD >= 2) {
+#pragma unroll
+            for (int k = 0; k < RW; ++k) xn[k] = xnn[k];
+            if (rn + step < r1) load_x(xnn, rn + step);
+        } else if (more) {
+            load_x(xn, rn);
+        }
+        const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
+        // chunk c's register is reloaded with the next batch's as soon as it
+        // has been used (one set of multiplier registers)
+#pragma unroll
+        for (int c = 0; c < NM; ++c) {
+            if (c < nch)                         // wave-uniform
+                dp_chunk4(x, m[c], sp[4 * c][lane], sp[4 * c + 1][lane], sp[4 * c + 2][lane],
+                          sp[4 * c + 3][lane]);
+            if (more) m[c] = load_m(rn, c);
+        }
+        // a row that was pivot row s of the group holds P[s] after pivot s
+        // and then takes the later pivots only: recomputed from P (rare --
+        // the chunks above gave it a meaningless value)
+        const long long R = sr[lane % NB];
+        if (__builtin_expect(__ballot(R >= rb && R < rb + RW) != 0, 0)) {
+#pragma unroll
+            for (int k = 0; k < RW; ++k) {
+                const long long row = rb + min(k, kmax);
+                int sl = -1;
+                for (int s = 0; s < nd; ++s)
+                    if (sr[s] == row) sl = s;
+                if (sl >= 0) {
+                    double2 y = sp[sl][lane];
+                    for (int s = sl + 1; s < nd; ++s) {
+                        const double f = M[s * rows + row];
+                        const double2 pv = sp[s][lane];
+                        y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
+                    }
+                    x[k] = y;
+                }
+            }
+        }
+        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(Tos + rb * ld);
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
+    }
+}
+
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
 // into rank p's summary slot, then every lane waits for rank p's granule in
 // the local buffer (bounded)
@@ -2151,6 +2297,24 @@ static int sweep_cus()
     return ncu;
 }
 
+// resident sweep workgroups per CU: the runtime's occupancy answer for the
+// compiled kernel (cached per kernel)
+static int sweep_blocks_per_cu(const void *fn, int threads)
+{
+    static std::mutex mu;
+    static std::map<const void *, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(fn);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, 0) != hipSuccess || n < 1) {
+        (void)hipGetLastError();
+        n = 1;
+    }
+    cache[fn] = n;
+    return n;
+}
+
 // The sweep: k_sweep_st (8 waves x 4-row batches), write-through (sc1)
 // stores -- the tableau lines leave the L2 as they are written instead of in
 // the writeback at the kernel's end (sweep 104-106 vs 106.5-108.4 us per
@@ -2165,7 +2329,46 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         const char *v = std::getenv("LPGPU_SWEEP_WIDE");
         wide = v ? std::atoi(v) : 0;
     }
+    static int dpp = -1;    // A/B: the DPP-broadcast sweep (k_sweep_dp)
+    if (dpp < 0) {
+        const char *v = std::getenv("LPGPU_SWEEP_DP");
+        dpp = v ? std::atoi(v) : 1;
+    }
     const long long ns = (A.ld + 127) / 128;
+    if (dpp) {
+        const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
+        const void *fn;
+        int wv = 8;
+        if (dpp >= 2) {   // two batches in flight, 6-wave workgroups (3 waves per SIMD)
+            wv = 6;
+            fn = nb == 16 ? (const void *)&k_sweep_dp<6, 16, SA, 2>
+               : nb == 32 ? (const void *)&k_sweep_dp<6, 32, SA, 2>
+               : nb == 48 ? (const void *)&k_sweep_dp<6, 48, SA, 2>
+                          : (const void *)&k_sweep_dp<6, 64, SA, 2>;
+        } else {
+            fn = nb == 16 ? (const void *)&k_sweep_dp<8, 16, SA, 1>
+               : nb == 32 ? (const void *)&k_sweep_dp<8, 32, SA, 1>
+               : nb == 48 ? (const void *)&k_sweep_dp<8, 48, SA, 1>
+                          : (const void *)&k_sweep_dp<8, 64, SA, 1>;
+        }
+        const int bpc = sweep_blocks_per_cu(fn, 64 * wv);
+        long long nrun = (long long)sweep_cus() * bpc / ns;
+        if (nrun < 1) nrun = 1;
+        long long run = (A.rows + nrun - 1) / nrun;
+        run = (run + RW - 1) / RW * RW;
+        nrun = (A.rows + run - 1) / run;
+        const dim3 grid((unsigned)(nrun * ns));
+        const Args *ap = &A;
+        const double *T = ap->T, *Pp = ap->P, *Mp = ap->M;
+        double *To = ap->T;
+        const long long *dRp = ap->dR;
+        const Ctl *ctlp = ap->ctl;
+        long long ld = ap->ld, rows = ap->rows;
+        int grpv = grp, nsv = (int)ns;
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run};
+        (void)hipExtLaunchKernel(fn, grid, dim3(64 * wv), args, 0, s, e0, e1, 0);
+        return hipGetLastError();
+    }
     int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
     if (wide && nd_max > 32) bpc = 1;
     long long nrun = (long long)sweep_cus() * bpc / ns;

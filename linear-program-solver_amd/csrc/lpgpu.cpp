@@ -42,7 +42,8 @@ struct lp_handle {
     double *T = nullptr, *P = nullptr, *M = nullptr, *row0 = nullptr, *col0 = nullptr;
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
-    int block = 32;                 // pivots deferred into one sweep (1..BMAX)
+    int block = 0;                  // pivots deferred into one sweep (1..BMAX; 0 = auto)
+    int block_auto = 0;             // the auto choice for this handle's shape (0: not yet made)
     bool persistent = true;         // one k_group launch per group where the shape fits
     int fallbacks = 0;              // timed-out persistent groups redone on the per-pivot kernels
     long long *stamps = nullptr;    // diagnostic phase clocks (LPGPU_STAMPS=1)
@@ -250,6 +251,7 @@ struct GroupComm : Comm {
 };
 
 static Members members_of(lp_handle *h) { return h->comm ? h->comm->members(h) : Members{h}; }
+static int block_of(lp_handle *h);
 
 // a multi-process shard: the scans combine every rank's per-column results
 // through an all-gather (RcclComm::gather_host)
@@ -633,6 +635,7 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     HCHK(h, hipDeviceSynchronize());
     if (!ok) return fail(h, LP_DEVICE_ERROR, "peer exchange check timed out");
     h->peer_ok = true;
+    h->block_auto = 0;                      // the exchange changes the selection's placement
     const unsigned bits = ((unsigned)ok >> 1) & 0xffu;
     h->share = 1;
     while (h->share < 8 && (bits >> h->share)) ++h->share;
@@ -649,6 +652,7 @@ extern "C" int lp_peer_enable(lp_handle *h, int enable)
         if (x) {
             if (enable && !x->dpeer) return fail(h, LP_BAD_ARG, "no peer exchange set up");
             x->peer_ok = enable != 0;
+            x->block_auto = 0;
         }
     return LP_PIVOTED;
 }
@@ -780,8 +784,8 @@ extern "C" int lp_upload_rows(lp_handle *h, int64_t row0, int64_t nrows, const d
 
 extern "C" int lp_set_block(lp_handle *h, int pivots_per_sweep)
 {
-    if (pivots_per_sweep < 1 || pivots_per_sweep > lpk::BMAX)
-        return fail(h, LP_BAD_ARG, "pivots_per_sweep must be in [1, 64]");
+    if (pivots_per_sweep < 0 || pivots_per_sweep > lpk::BMAX)
+        return fail(h, LP_BAD_ARG, "pivots_per_sweep must be in [1, 64], or 0 (auto)");
     for (lp_handle *x : members_of(h))
         if (x) x->block = pivots_per_sweep;
     return LP_PIVOTED;
@@ -789,7 +793,7 @@ extern "C" int lp_set_block(lp_handle *h, int pivots_per_sweep)
 
 extern "C" int lp_get_block(const lp_handle *h, int *pivots_per_sweep)
 {
-    *pivots_per_sweep = h->block;
+    *pivots_per_sweep = block_of(const_cast<lp_handle *>(h));
     return LP_PIVOTED;
 }
 
@@ -846,7 +850,7 @@ static int launch_sweep_timed(lp_handle *h, const Args &A, int grp)
 {
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 0));
-    HCHK(h, lpk::launch_sweep(h->s, A, grp, h->block, e0, e1));
+    HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), e0, e1));
     return LP_PIVOTED;
 }
 
@@ -868,7 +872,7 @@ static int launch_group_timed(lp_handle *h, const Args &A, const lpk::GroupGeom 
     CALL(prof_slot(h, &e0, &e1, 1));
     Args a = A;
     if (h->fault_launch > 0 && (unsigned)h->fault_launch == h->gseq) a.fault = h->fault_t + 1;
-    HCHK(h, lpk::launch_group(h->s, a, geo, grp, cnt, from_erec, h->gseq, h->block, xr, As, nshard,
+    HCHK(h, lpk::launch_group(h->s, a, geo, grp, cnt, from_erec, h->gseq, block_of(h), xr, As, nshard,
                               cs.first, cs.mode, cs.rule, cs.cap, e0, e1));
     return LP_PIVOTED;
 }
@@ -883,16 +887,46 @@ static int launch_group_timed(lp_handle *h, const Args &A, const lpk::GroupGeom 
 //   whose queue is not mapped never answers: measured, round 1) -- else one
 //   collective per pivot.  Every rank decides from the same values (global
 //   sizes, the ping's shared-GPU count), so all take the same path.
-static lpk::GroupGeom persistent_geom(lp_handle *h, const Members &M, int *xr)
+static lpk::GroupGeom persistent_geom_b(lp_handle *h, size_t nmem, int *xr, int bmax)
 {
     *xr = 0;
     lpk::GroupGeom none;
     if (!h->persistent) return none;
-    if (!h->comm) return lpk::group_geom(h->rc, h->ld, h->block, 0, 1, 1);
+    if (!h->comm) return lpk::group_geom(h->rc, h->ld, bmax, 0, 1, 1);
     if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
-    *xr = (M.size() == 1 && h->xr_xcd) ? 2 : 1;
-    return lpk::group_geom(rcmax, h->ld, h->block, *xr, (int)M.size(), M.size() == 1 ? h->share : 1);
+    *xr = (nmem == 1 && h->xr_xcd) ? 2 : 1;
+    return lpk::group_geom(rcmax, h->ld, bmax, *xr, (int)nmem, nmem == 1 ? h->share : 1);
+}
+
+// Pivots per sweep when the handle says auto (0).  More pivots per sweep cut
+// the sweep's traffic per pivot, but each selection block keeps its rows'
+// multipliers and its columns' pivot-row values in LDS, so past some depth
+// the persistent selection no longer fits on one XCD (its L2-resident
+// hand-offs) and gets slower: the deepest of 64 / 48 / 32 whose selection
+// still runs on one XCD; 64 where none does (a tall shard spread over the
+// device anyway: cfg4 on one GPU, 31.6-32.0k pivots/s at 64 against 28.8k at
+// 48); 32 on the per-pivot kernels.  cfg3 (4096 x 8192): 48, 100-101k
+// against 97-98k at 32 and 80k at 64 (profiles/r02/README.md).  Every rank
+// of a sharded job decides from the same global sizes.
+static int block_of(lp_handle *h)
+{
+    if (h->block > 0) return h->block;
+    if (h->block_auto > 0) return h->block_auto;
+    const size_t nmem = h->comm ? std::max<size_t>(members_of(h).size(), 1) : 1;
+    int xr = 0, pick = 0;
+    for (int b : {64, 48, 32}) {
+        const lpk::GroupGeom g = persistent_geom_b(h, nmem, &xr, b);
+        if (g.g > 0 && g.xmode) { pick = b; break; }
+    }
+    if (!pick) pick = persistent_geom_b(h, nmem, &xr, 64).g > 0 ? 64 : 32;
+    h->block_auto = pick;
+    return pick;
+}
+
+static lpk::GroupGeom persistent_geom(lp_handle *h, const Members &M, int *xr)
+{
+    return persistent_geom_b(h, M.size(), xr, block_of(h));
 }
 
 // one persistent selection launch per rank for a group of cnt pivots.  The
@@ -1105,9 +1139,9 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         CALL(begin_call(M, A, mode, rule, 1, cap, -1, -1));
         for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
     }
-    const int B = h->block;
+    const int B = block_of(h);
     int64_t done = 0;      // pivots performed (device count)
-    int64_t batch = 8 * B;
+    int64_t batch = 2 * B;   // open-ended solves: few launches for a short solve, then doubling
     int grp = 0;
     bool chained = false;  // the next pivot's entering column comes from the previous pivot
     unsigned first_seq = 0;

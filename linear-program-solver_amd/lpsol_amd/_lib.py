@@ -308,10 +308,11 @@ class Engine:
         return p.value, f.value
 
     def set_block(self, pivots_per_sweep: int):
-        """pivots deferred into one sweep of the tableau (1..64)"""
+        """pivots deferred into one sweep of the tableau (1..64; 0 = auto)"""
         self._check(self.lib.lp_set_block(self.h, int(pivots_per_sweep)), self.h)
 
     def get_block(self) -> int:
+        """pivots per sweep in use (the auto choice resolved)"""
         b = C.c_int()
         self.lib.lp_get_block(self.h, C.byref(b))
         return b.value

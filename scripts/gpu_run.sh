@@ -208,7 +208,8 @@ for step in "$@"; do
             for W in ${PMC_WORKLOADS:-cfg4 cfg3}; do
                 run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
                 run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
-                run pmc_json_$W 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch_$W" "$OUT/pmc_write_$W" profiles/r02/hbm_traffic.json --block 32 --kernel k_sweep_st --workload $W
+                PB=$([ "$W" = cfg4 ] && echo 64 || echo 48)   # the engine's auto pivots per sweep
+                run pmc_json_$W 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch_$W" "$OUT/pmc_write_$W" profiles/r02/hbm_traffic.json --block $PB --kernel k_sweep_dp --workload $W
             done
             cp profiles/r02/hbm_traffic.json "$OUT/hbm_traffic.json" ;;
         proffinal)
@@ -245,6 +246,24 @@ for step in "$@"; do
             LPGPU_LIB=$L run stamps_cfg4_p 300 python scripts/diag_stamps.py tall 32768 8192 32
             LPGPU_LIB=$L run stamps_cfg3_p 300 python scripts/diag_stamps.py mixed 4096 4096 32
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_cfg*_p_b*.log "$OUT"/bench_cfg*_raw_b*.log ;;
+        exp4)
+            LPGPU_SWEEP_DP=1 run pytest_dp 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for B in 32 48 64; do
+                LPGPU_SWEEP_DP=1 run bench_cfg4_dp_b$B 300 python bench.py --no-cpu-baseline --no-cfg3 --block $B --steps 24 --warmup 4
+                LPGPU_SWEEP_DP=1 run bench_cfg3_dp_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --block $B --steps 64 --warmup 4
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_cfg*_dp_b*.log ;;
+        exp5)
+            LPGPU_SWEEP_DP=2 run pytest_dp2 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_r2.py -k "block_size or cfg3_full or cfg4 or ragged" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for D in 1 2; do
+                for B in 48 64; do
+                    LPGPU_SWEEP_DP=$D run bench_cfg4_d${D}_b$B 300 python bench.py --no-cpu-baseline --no-cfg3 --block $B --steps 24 --warmup 4
+                done
+                for B in 32 48; do
+                    LPGPU_SWEEP_DP=$D run bench_cfg3_d${D}_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --block $B --steps 64 --warmup 4
+                done
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_cfg*_d*_b*.log ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

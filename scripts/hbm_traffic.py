@@ -1,4 +1,4 @@
-"""HBM bytes per sweep (k_sweep_st) launch from two rocprofv3 --pmc passes.
+"""HBM bytes per sweep (k_sweep_dp) launch from two rocprofv3 --pmc passes.
 
 FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950 (TCC slots), so
 scripts/gpu_run.sh runs bench.py twice under rocprofv3, once per counter.
@@ -45,7 +45,7 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("out")
     ap.add_argument("--block", type=int, default=16)
-    ap.add_argument("--kernel", default="k_sweep_st")
+    ap.add_argument("--kernel", default="k_sweep_dp")
     ap.add_argument("--workload", default="cfg4")
     a = ap.parse_args()
     import bench
