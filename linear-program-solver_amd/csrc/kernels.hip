@@ -747,11 +747,12 @@ __device__ __forceinline__ void stamp(const Args &A, unsigned b, int t, int k)
     if (A.stamps && b == 0 && threadIdx.x == 0 && t < BMAX)
         *gp(A.stamps + t * 16 + k) = (long long)__builtin_amdgcn_s_memrealtime();
 }
-// every block: when it published its ratio (k = 0) / row-0 (k = 1) summary
+// every block: when it published its ratio (k = 0) / row-0 (k = 1) summary,
+// knew the entering column (k = 2), had its column elements (k = 3)
 __device__ __forceinline__ void bstamp(const Args &A, unsigned b, int t, int k)
 {
     if (A.stamps && threadIdx.x == 0 && t < BMAX)
-        *gp(A.stamps + BMAX * 16 + (b * BMAX + t) * 2 + k) = (long long)__builtin_amdgcn_s_memrealtime();
+        *gp(A.stamps + BMAX * 16 + (b * BMAX + t) * 4 + k) = (long long)__builtin_amdgcn_s_memrealtime();
 }
 #else
 constexpr bool STAMPS = false;
@@ -1235,6 +1236,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             if (C == NONE) status = halt ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
         stamp(A, b, t, 1);
+        bstamp(A, b, t, 2);
         if (pending >= 0) {
 #pragma unroll
             for (int k = 0; k < RPL; ++k)
@@ -1259,6 +1261,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         }
         __syncthreads();
         stamp(A, b, t, 3);
+        if (STAMPS && A.stamps) {   // diagnostic: the column elements have arrived
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bstamp(A, b, t, 3);
+        }
         // deferred pivots 0..t-1 on the own rows' elements of column C, CH at
         // a time.  A lane whose row was an earlier pivot row takes the select;
         // otherwise plain FMAs.
@@ -1919,26 +1925,29 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
 //   identical to k_sweep_st and oracle/lp_f64.c.
 // ---------------------------------------------------------------------------
 
-// pivots 4c .. 4c + 3 of one batch (4 rows x 2 columns per lane): 32 FMAs
-// whose multiplier operand is lane (4 s' + k) of the lane's 16-lane row of m.
-// The s_nop covers the VALU-write -> DPP-read hazard should the compiler copy
-// m into place right before the block.
-__device__ __forceinline__ void dp_chunk4(double2 (&x)[4], double m, double2 p0, double2 p1, double2 p2,
-                                          double2 p3)
-{
+// pivots 4c + 2h, 4c + 2h + 1 of one batch (4 rows x 2 columns per lane): 16
+// FMAs whose multiplier operand is lane (4 s' + k) of the lane's 16-lane row
+// of m.  The s_nop (first half only) covers the VALU-write -> DPP-read hazard
+// should the compiler copy m into place right before the block.
 #define DPF(XR, PV, L) "v_fmac_f64_dpp " XR ", -%8, " PV " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
 #define DPP_PIVOT(L0, L1, L2, L3, PX, PY)                                                     \
     DPF("%0", PX, L0) DPF("%1", PY, L0) DPF("%2", PX, L1) DPF("%3", PY, L1) DPF("%4", PX, L2) \
     DPF("%5", PY, L2) DPF("%6", PX, L3) DPF("%7", PY, L3)
-    asm volatile("s_nop 1\n" DPP_PIVOT(0, 1, 2, 3, "%9", "%10") DPP_PIVOT(4, 5, 6, 7, "%11", "%12")
-                     DPP_PIVOT(8, 9, 10, 11, "%13", "%14") DPP_PIVOT(12, 13, 14, 15, "%15", "%16")
-                 : "+v"(x[0].x), "+v"(x[0].y), "+v"(x[1].x), "+v"(x[1].y), "+v"(x[2].x), "+v"(x[2].y),
-                   "+v"(x[3].x), "+v"(x[3].y)
-                 : "v"(m), "v"(p0.x), "v"(p0.y), "v"(p1.x), "v"(p1.y), "v"(p2.x), "v"(p2.y), "v"(p3.x),
-                   "v"(p3.y));
+#define DPP_OUTS(x)                                                                                       \
+    "+v"(x[0].x), "+v"(x[0].y), "+v"(x[1].x), "+v"(x[1].y), "+v"(x[2].x), "+v"(x[2].y), "+v"(x[3].x), \
+        "+v"(x[3].y)
+__device__ __forceinline__ void dp_half(double2 (&x)[4], double m, double2 p0, double2 p1, int h)
+{
+    if (h == 0)
+        asm("s_nop 1\n" DPP_PIVOT(0, 1, 2, 3, "%9", "%10") DPP_PIVOT(4, 5, 6, 7, "%11", "%12")
+            : DPP_OUTS(x) : "v"(m), "v"(p0.x), "v"(p0.y), "v"(p1.x), "v"(p1.y));
+    else
+        asm(DPP_PIVOT(8, 9, 10, 11, "%9", "%10") DPP_PIVOT(12, 13, 14, 15, "%11", "%12")
+            : DPP_OUTS(x) : "v"(m), "v"(p0.x), "v"(p0.y), "v"(p1.x), "v"(p1.y));
+}
+#undef DPP_OUTS
 #undef DPP_PIVOT
 #undef DPF
-}
 
 template <int W, int NB, int SA, int PD>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PD >= 2 ? 3 : 4, 8)))
@@ -2013,11 +2022,20 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
         const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
         // chunk c's register is reloaded with the next batch's as soon as it
         // has been used (one set of multiplier registers)
+        // the next pivot pair's P is read from LDS while this pair's FMAs run
+        double2 pa = sp[0][lane], pb = sp[1][lane];
 #pragma unroll
         for (int c = 0; c < NM; ++c) {
-            if (c < nch)                         // wave-uniform
-                dp_chunk4(x, m[c], sp[4 * c][lane], sp[4 * c + 1][lane], sp[4 * c + 2][lane],
-                          sp[4 * c + 3][lane]);
+            if (c < nch) {                       // wave-uniform
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int s2 = 4 * c + 2 * h + 2;
+                    const double2 qa = sp[s2 < NB ? s2 : 0][lane], qb = sp[s2 + 1 < NB ? s2 + 1 : 1][lane];
+                    dp_half(x, m[c], pa, pb, h);
+                    pa = qa;
+                    pb = qb;
+                }
+            }
             if (more) m[c] = load_m(rn, c);
         }
         // a row that was pivot row s of the group holds P[s] after pivot s

@@ -376,7 +376,7 @@ static int alloc_handle(lp_handle *h)
     if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
-            const size_t sb = (lpk::BMAX * 16 + lpk::GROUP_MAXBLOCKS * lpk::BMAX * 2) * sizeof(long long);
+            const size_t sb = (lpk::BMAX * 16 + lpk::GROUP_MAXBLOCKS * lpk::BMAX * 4) * sizeof(long long);
             HCHK(h, hipMalloc(&h->stamps, sb));
             HCHK(h, hipMemset(h->stamps, 0, sb));
         }
@@ -1602,7 +1602,7 @@ extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
 {
     if (!h->stamps) return LP_BAD_ARG;
     HCHK(h, hipMemcpy(out, h->stamps + lpk::BMAX * 16,
-                      lpk::GROUP_MAXBLOCKS * lpk::BMAX * 2 * sizeof(long long), hipMemcpyDeviceToHost));
+                      lpk::GROUP_MAXBLOCKS * lpk::BMAX * 4 * sizeof(long long), hipMemcpyDeviceToHost));
     return LP_PIVOTED;
 }
 

@@ -39,21 +39,33 @@ sub = [[(buf[t * 16 + 12] - buf[t * 16 + 8]) / 100, (buf[t * 16 + 13] - buf[t * 
         (buf[t * 16 + 9] - buf[t * 16 + 13]) / 100] for t in range(1, NT)]
 print("pcomp split: chain=%.2f div=%.2f store=%.2f" % tuple(sum(x[i] for x in sub) / len(sub) for i in range(3)))
 
-# per-block publish times: spread across blocks and the last blocks
-bb = (C.c_longlong * (256 * BMAX * 2))()
+# per-block event times (every block): C known (2), column loaded (3), ratio
+# summary published (0), row-0 summary published (1); spread = last - first
+bb = (C.c_longlong * (256 * BMAX * 4))()
 assert e.lib.lpdiag_bstamps(e.h, bb) == 0
-spread = [[], []]
+ev = {2: "C known", 3: "column loaded", 0: "ratio published", 1: "row0 published"}
+sp = {k: [] for k in ev}
 last = {}
+rel = {k: [] for k in ev}   # mean time of the event after the pivot's earliest 'C known'
 for t in range(1, NT):
-    for k in (0, 1):
-        v = [bb[(b * BMAX + t) * 2 + k] for b in range(256)]
+    base = [bb[(b * BMAX + t) * 4 + 2] for b in range(256)]
+    base = [x for x in base if x]
+    if not base:
+        continue
+    t0 = min(base)
+    for k in ev:
+        v = [bb[(b * BMAX + t) * 4 + k] for b in range(256)]
         v = [x for x in v if x]
         if not v:
             continue
-        spread[k].append((max(v) - min(v)) * 10 / 1000)
-        order = sorted(range(len(v)), key=lambda i: v[i])
-        for b in order[-3:]:
-            last[(k, b)] = last.get((k, b), 0) + 1
-print("publish spread us: ratio avg %.2f max %.2f | row0 avg %.2f max %.2f" % (
-    sum(spread[0]) / len(spread[0]), max(spread[0]), sum(spread[1]) / len(spread[1]), max(spread[1])))
-print("most often among the last 3:", sorted(last.items(), key=lambda kv: -kv[1])[:10])
+        sp[k].append((max(v) - min(v)) * 10 / 1000)
+        rel[k].append(((sum(v) / len(v)) - t0) * 10 / 1000)
+        if k == 0:
+            order = sorted(range(len(v)), key=lambda i: v[i])
+            for b in order[-3:]:
+                last[b] = last.get(b, 0) + 1
+for k in (2, 3, 0, 1):
+    if sp[k]:
+        print("%-16s spread avg %.2f max %.2f us | mean after first C-known %.2f us" % (
+            ev[k], sum(sp[k]) / len(sp[k]), max(sp[k]), sum(rel[k]) / len(rel[k])))
+print("most often among the last 3 ratio publishers:", sorted(last.items(), key=lambda kv: -kv[1])[:10])

@@ -264,6 +264,20 @@ for step in "$@"; do
                 done
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*' "$OUT"/bench_cfg*_d*_b*.log ;;
+        pmcsq2)
+            export TMPDIR=/tmp
+            for W in cfg3 cfg4; do
+                run pmcsq_$W 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_LDS --output-format csv -d "$OUT/pmcsq_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 16 --warmup 4 --no-cpu-baseline
+                run pmcsq2_$W 300 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcsq2_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 16 --warmup 4 --no-cpu-baseline
+            done ;;
+        quick)
+            # parity subset + cfg4 / cfg3 timing (auto pivots per sweep)
+            run pytest_quick 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_r2.py -k "block_size or cfg3_full or cfg4 or ragged" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2; do
+                run bench_q4_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                run bench_q3_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
+            done
+            grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_q*.log ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
