@@ -278,6 +278,13 @@ for step in "$@"; do
                 run bench_q3_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
             done
             grep -H -o '"value": [0-9.]*\|"avg_launch_us": [0-9.]*\|"us_per_pivot": [0-9.]*' "$OUT"/bench_q*.log ;;
+        full)
+            # whole GPU suite (stops at the first failure), then the quick timing
+            run pytest_full 1000 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        stamps2)
+            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
+            LPGPU_LIB=$L run stamps2_cfg4 300 python scripts/diag_stamps.py tall 32768 8192 64
+            LPGPU_LIB=$L run stamps2_cfg3 300 python scripts/diag_stamps.py mixed 4096 4096 48 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
