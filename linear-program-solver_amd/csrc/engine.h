@@ -128,10 +128,10 @@ struct Args {
     long long rb;        // first global constraint row of this rank
     long long rc;        // local constraint rows
     int nranks;
-    int pad;
+    int gmaj;            // k_group: granule-major summaries when on one XCD (1, default) or never (0)
     lp_tol tol;
     long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
-    unsigned long long *gran;  // k_group summaries: 3 phases (ratio, row 0, XCD check) x GROUP_MAXBLOCKS x 8 tagged granules
+    unsigned long long *gran;  // k_group summaries: 3 regions (ratio, row 0, XCD check) x GROUP_MAXBLOCKS x 8 tagged granules
     unsigned spin_max;   // k_group: polls of one exchange before it gives up (timeout)
     unsigned xwait_ms;   // k_group (XR): wall-clock bound of a cross-rank wait
     int fault;           // tests only (LPGPU_FAULT): t + 1 -> block 1 withholds pivot t's ratio summary

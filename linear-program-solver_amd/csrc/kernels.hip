@@ -794,11 +794,33 @@ __device__ __forceinline__ void st_x(T *p, T v, bool fast)
     else st_sc1(p, v);
 }
 
-// lanes 0..n-1 store word[lane] of this block's summary (after the drain)
-__device__ __forceinline__ void publish(u64 *slot, unsigned tag, unsigned w, int n, bool fast)
+// Summary regions are granule-major: granule g of block b at [g * GROUP_MAXBLOCKS + b],
+// so one poll instruction (granule g of 64 consecutive blocks) reads 512
+// contiguous bytes -- 4 cache lines instead of 32-64 with block-major slots.
+// Every block polls every summary until all have arrived, so the poll
+// traffic is G x lines per instruction x NG per round: block-major, 64
+// blocks polling 8-granule summaries asked an XCD's L2 for several times
+// the lines its 16 channels serve per cycle, and every other access of the
+// selection (the publications themselves, the column and row loads) queued
+// behind the polls.
+// That layout is for blocks on ONE XCD (xs = 0).  Blocks spread over the XCDs
+// (xs = 1) keep block-major 64-byte slots (two consecutive blocks, on two
+// XCDs, per line): there the stores matter -- write-through partial-line
+// stores from several XCDs into one line serialise (granule-major: selection
+// 14.4 -> 16.3 us per pivot at cfg4; granule rows grouped by XCD: 18.7), and
+// so does pairing two blocks of one XCD in a line (16.0-17.0) or giving each
+// block a whole line (more lines per poll: 16.9-18.7) (profiles/r02/README.md).
+constexpr int GSLOT = 8;    // granules per block slot, block-major
+__device__ __forceinline__ unsigned gslot(int g, unsigned b, int xs)
+{
+    return xs ? b * GSLOT + g : g * GROUP_MAXBLOCKS + b;
+}
+// lanes 0..n-1 store word[lane] of block b's summary (after the drain)
+__device__ __forceinline__ void publish(u64 *region, unsigned b, unsigned tag, unsigned w, int n, bool fast,
+                                        int xs)
 {
     drain_stores();
-    if ((int)threadIdx.x < n) st_x(&slot[threadIdx.x], ((u64)tag << 32) | w, fast);
+    if ((int)threadIdx.x < n) st_x(&region[gslot(threadIdx.x, b, xs)], ((u64)tag << 32) | w, fast);
 }
 
 // every block's summary, lane l holding blocks l + 64k; polls until every
@@ -807,9 +829,9 @@ __device__ __forceinline__ void publish(u64 *slot, unsigned tag, unsigned w, int
 // (Keeping a second poll in flight was measured: the gather ends sooner but
 // the leftover loads delay the next phase's loads by as much -- vmcnt retires
 // in order.)
-template <int NR, int NG>
+template <int NR, int NG, bool GMAJ = true>
 __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[NR][NG],
-                       unsigned *timeout_flag, unsigned spin_max)
+                       unsigned *timeout_flag, unsigned spin_max, int xs = 0)
 {
     for (unsigned spins = 0;; ++spins) {
         // every load is issued before any is waited for: lanes past the last
@@ -820,7 +842,7 @@ __device__ bool gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[
             const unsigned bb = min(threadIdx.x + k * GROUP_THREADS, G - 1);
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
-                const u64 v = ld_sc1(&base[bb * 8 + g]);
+                const u64 v = ld_sc1(GMAJ ? &base[gslot(g, bb, xs)] : &base[bb * 8 + g]);
                 w[k][g] = (unsigned)v;
                 ok = ok && (unsigned)(v >> 32) == tag;
             }
@@ -1028,15 +1050,17 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         st_sc1(&ctl->g_rule, rule);
         st_sc1(&ctl->g_seq, seq);
     }
-    u64 *grR = A.gran;                         // ratio summaries [G][8]
-    u64 *grE = A.gran + GROUP_MAXBLOCKS * 8;   // row-0 summaries [G][8]
+    // summary regions of GROUP_MAXBLOCKS x GSLOT granules: ratio, row 0, XCD check
+    u64 *grR = A.gran;
+    u64 *grE = A.gran + GROUP_MAXBLOCKS * GSLOT;
+    const int xs = (xmode && A.gmaj) ? 0 : 1;  // 0: granule-major (one XCD), 1: block-major
     bool fast = false;
     if (xmode) {
         // every block publishes its XCD; plain hand-off stores only if all match
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-        u64 *grX = A.gran + 2 * GROUP_MAXBLOCKS * 8;
-        if (threadIdx.x == 0) st_sc1(&grX[b * 8], ((u64)gtag(seq, 0, 7) << 32) | xcc);
+        u64 *grX = A.gran + 2 * GROUP_MAXBLOCKS * GSLOT;
+        if (threadIdx.x == 0) st_sc1(&grX[gslot(0, b, 0)], ((u64)gtag(seq, 0, 7) << 32) | xcc);
         unsigned wx[NRMAX][1];
         if (!gather<NRMAX, 1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
             if (b == 0 && threadIdx.x == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
@@ -1182,10 +1206,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     else if (tid == 3) wv = hi32(seq_);
                     else if (tid == 4) wv = idx32(sei_);
                     else if (tid == 5) wv = idx32(sfn_) & 0x7fffffffu;
-                    publish(&grE[b * 8], etag, wv, NGE, fast);
+                    publish(grE, b, etag, wv, NGE, fast, xs);
                 }
                 unsigned w[NR][NGE];
-                if (!gather<NR, NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max)) {
+                if (!gather<NR, NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max, xs)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -1343,7 +1367,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 3) wv = hi32(qb);
             else if (tid == 5) wv = lo32(ab);
             else if (tid == 6) wv = hi32(ab);
-            publish(&grR[b * 8], gtag(seq, t, 0), wv, NGRX, fast);
+            publish(grR, b, gtag(seq, t, 0), wv, NGRX, fast, xs);
         }
         bstamp(A, b, t, 0);
         stamp(A, b, t, 5);
@@ -1352,7 +1376,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         double rl[NR];
         double rmin = INFINITY;
         unsigned w[NR][NGRX];
-        if (!gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max)) {
+        if (!gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max, xs)) {
             status = LP_DEVICE_ERROR;
             break;
         }
@@ -1548,7 +1572,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                         st_sc1(&loc[b * 8 + tid], ((u64)gtag(seq, t, 4) << 32) | wv);
                     }
                     unsigned wl[NR][3];
-                    if (!gather<NR, 3>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout, A.spin_max)) {
+                    if (!gather<NR, 3, false>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout, A.spin_max)) {
                         status = LP_DEVICE_ERROR;
                         break;
                     }
@@ -1687,7 +1711,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 5) wv = (idx32(efn) & 0x7fffffffu) | ((unsigned)rule << 31);
             else if (tid == 6) wv = lo32(p0n);
             else if (tid == 7) wv = hi32(p0n);
-            publish(&grE[b * 8], gtag(seq, t, 1), wv, NGE, fast);
+            publish(grE, b, gtag(seq, t, 1), wv, NGE, fast, xs);
         }
         // records read after the launch only (host, sweep, next launch): one
         // store instruction of the last block (block 0 already carries the
@@ -1725,7 +1749,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     // row-0 summary
     if (pending >= 0) {
         unsigned w[NR][NGE];
-        if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout, A.spin_max)) {
+        if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout, A.spin_max, xs)) {
             const double pl = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
                                    __builtin_amdgcn_readfirstlane(w[0][7]));
 #pragma unroll

@@ -287,11 +287,15 @@ static Args args_of(const lp_handle *h)
     A.m = h->m;
     A.n = h->n;
     A.ld = h->ld;
+    static const int gmaj = [] {
+        const char *v = std::getenv("LPGPU_GMAJ");   // A/B: 0 = block-major summaries always
+        return v ? std::atoi(v) : 1;
+    }();
+    A.gmaj = gmaj;
     A.rows = h->rows;
     A.rb = h->rb;
     A.rc = h->rc;
     A.nranks = h->nranks;
-    A.pad = 0;
     A.tol = h->tol;
     A.stamps = h->stamps;
     A.gran = h->gran;
@@ -391,7 +395,7 @@ static int alloc_handle(lp_handle *h)
     const size_t mbytes = 2 * ((size_t)lpk::BMAX * h->rows + lpk::M_PAD) * sizeof(double);
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
-    const size_t gbytes = 3 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
+    const size_t gbytes = 3 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);   // k_group summary regions
     HCHK(h, hipMalloc(&h->gran, gbytes));
     HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
     HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));

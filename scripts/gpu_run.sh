@@ -285,6 +285,18 @@ for step in "$@"; do
             L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
             LPGPU_LIB=$L run stamps2_cfg4 300 python scripts/diag_stamps.py tall 32768 8192 64
             LPGPU_LIB=$L run stamps2_cfg3 300 python scripts/diag_stamps.py mixed 4096 4096 48 ;;
+        abq)
+            # A/B: variants/headA.so against the current build (LPGPU_GMAJ 1 / 0), cfg4 and cfg3
+            for rep in 1 2; do
+                for V in headA cur cur0; do
+                    L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/headA.so
+                    [ $V = headA ] || L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/liblpgpu.so
+                    G=1; [ $V = cur0 ] && G=0
+                    LPGPU_LIB=$L LPGPU_GMAJ=$G run ab4_${V}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                    LPGPU_LIB=$L LPGPU_GMAJ=$G run ab3_${V}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
+                done
+            done
+            for f in "$OUT"/ab*_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"us_per_pivot": [0-9.]*' $f | tail -1)"; done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
