@@ -1909,7 +1909,7 @@ __device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)
 // LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt,
 // 16 sc1 = write-through)
 template <int W, int RW, int NB, int LA = 0, int SA = 0>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >= 16 ? 4 : NB <= 32 ? 6 : 2, 8)))
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(NB <= 32 ? 6 : 2, 8)))
 k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
            const double *__restrict__ M, const long long *__restrict__ dR,
            const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
@@ -1973,8 +1973,8 @@ __device__ __forceinline__ void dp_half(double2 (&x)[4], double m, double2 p0, d
 #undef DPP_PIVOT
 #undef DPF
 
-template <int W, int NB, int SA, int PD>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(PD >= 2 ? 3 : 4, 8)))
+template <int W, int NB, int SA>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
            int nstrips, long long run)
@@ -2020,14 +2020,14 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
     };
     const long long step = (long long)W * RW;
     long long rb = r0 + (long long)wave * RW;
-    // PD batches of rows in flight ahead of the one being updated
-    double2 xn[RW], xnn[RW];
+    // the next batch's rows are in flight while the current one is updated
+    // (two batches ahead, 3 waves per SIMD: 5-25 % slower)
+    double2 xn[RW];
     double m[NM];                                // the current batch's multipliers
     if (rb < r1) {
         load_x(xn, rb);
 #pragma unroll
         for (int c = 0; c < NM; ++c) m[c] = load_m(rb, c);
-        if (PD >= 2 && rb + step < r1) load_x(xnn, rb + step);
     }
     __syncthreads();                             // sp, sr staged
     for (; rb < r1; rb += step) {
@@ -2036,13 +2036,7 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
         for (int k = 0; k < RW; ++k) x[k] = xn[k];
         const long long rn = rb + step;
         const bool more = rn < r1;
-        if (PD >= 2) {
-#pragma unroll
-            for (int k = 0; k < RW; ++k) xn[k] = xnn[k];
-            if (rn + step < r1) load_x(xnn, rn + step);
-        } else if (more) {
-            load_x(xn, rn);
-        }
+        if (more) load_x(xn, rn);
         const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
         // chunk c's register is reloaded with the next batch's as soon as it
         // has been used (one set of multiplier registers)
@@ -2366,11 +2360,6 @@ static int sweep_blocks_per_cu(const void *fn, int threads)
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0, hipEvent_t e1)
 {
     constexpr int W = 8, RW = 4, SA = 16;
-    static int wide = -1;   // A/B: 16-wave workgroups past 32 pivots
-    if (wide < 0) {
-        const char *v = std::getenv("LPGPU_SWEEP_WIDE");
-        wide = v ? std::atoi(v) : 0;
-    }
     static int dpp = -1;    // A/B: the DPP-broadcast sweep (k_sweep_dp)
     if (dpp < 0) {
         const char *v = std::getenv("LPGPU_SWEEP_DP");
@@ -2379,20 +2368,11 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
     const long long ns = (A.ld + 127) / 128;
     if (dpp) {
         const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
-        const void *fn;
-        int wv = 8;
-        if (dpp >= 2) {   // two batches in flight, 6-wave workgroups (3 waves per SIMD)
-            wv = 6;
-            fn = nb == 16 ? (const void *)&k_sweep_dp<6, 16, SA, 2>
-               : nb == 32 ? (const void *)&k_sweep_dp<6, 32, SA, 2>
-               : nb == 48 ? (const void *)&k_sweep_dp<6, 48, SA, 2>
-                          : (const void *)&k_sweep_dp<6, 64, SA, 2>;
-        } else {
-            fn = nb == 16 ? (const void *)&k_sweep_dp<8, 16, SA, 1>
-               : nb == 32 ? (const void *)&k_sweep_dp<8, 32, SA, 1>
-               : nb == 48 ? (const void *)&k_sweep_dp<8, 48, SA, 1>
-                          : (const void *)&k_sweep_dp<8, 64, SA, 1>;
-        }
+        const int wv = W;
+        const void *fn = nb == 16 ? (const void *)&k_sweep_dp<W, 16, SA>
+                       : nb == 32 ? (const void *)&k_sweep_dp<W, 32, SA>
+                       : nb == 48 ? (const void *)&k_sweep_dp<W, 48, SA>
+                                  : (const void *)&k_sweep_dp<W, 64, SA>;
         const int bpc = sweep_blocks_per_cu(fn, 64 * wv);
         long long nrun = (long long)sweep_cus() * bpc / ns;
         if (nrun < 1) nrun = 1;
@@ -2411,8 +2391,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         (void)hipExtLaunchKernel(fn, grid, dim3(64 * wv), args, 0, s, e0, e1, 0);
         return hipGetLastError();
     }
-    int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
-    if (wide && nd_max > 32) bpc = 1;
+    const int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
     long long nrun = (long long)sweep_cus() * bpc / ns;
     if (nrun < 1) nrun = 1;
     long long run = (A.rows + nrun - 1) / nrun;
@@ -2422,17 +2401,11 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
 #define SWEEP_ST_ONE(NBV)                                                                            \
     hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, 0, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, A.T, \
                           A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
-#define SWEEP_ST_WIDE(NBV)                                                                           \
-    hipExtLaunchKernelGGL((k_sweep_st<16, RW, NBV, 0, SA>), grid, dim3(64 * 16), 0, s, e0, e1, 0, A.T, A.T, \
-                          A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
-    if (wide && nd_max > 48) SWEEP_ST_WIDE(64);
-    else if (wide && nd_max > 32) SWEEP_ST_WIDE(48);
-    else if (nd_max <= 16) SWEEP_ST_ONE(16);
+    if (nd_max <= 16) SWEEP_ST_ONE(16);
     else if (nd_max <= 32) SWEEP_ST_ONE(32);
     else if (nd_max <= 48) SWEEP_ST_ONE(48);
     else SWEEP_ST_ONE(64);
 #undef SWEEP_ST_ONE
-#undef SWEEP_ST_WIDE
     return hipGetLastError();
 }
 
@@ -2489,6 +2462,11 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
         const char *v = std::getenv("LPGPU_SEL_XCD");
         xcd_on = v ? std::atoi(v) : 1;
     }
+    static long long gmin_env = -1;
+    if (gmin_env < 0) {
+        const char *v = std::getenv("LPGPU_SEL_BLOCKS");
+        gmin_env = v ? std::atoll(v) : 0;
+    }
     const int cus = sweep_cus(), xcd_cus = cus / 8;
     // candidate block counts, preferred first: at least one own row per
     // lane-slot, every lane at most 4 columns; with a few extra blocks every
@@ -2505,6 +2483,7 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
         for (int wide = 1; wide >= 0; --wide) {
             long long g = (rc + 64LL * rpl - 1) / (64LL * rpl);
             if (g < GROUP_MINBLOCKS) g = GROUP_MINBLOCKS;
+            if (gmin_env > g) g = gmin_env;   // A/B: more blocks than rows need
             const long long g2 = (ld + 2 * GROUP_THREADS - 1) / (2 * GROUP_THREADS);
             const long long g4 = (ld + 4 * GROUP_THREADS - 1) / (4 * GROUP_THREADS);
             if (wide && g2 > g && g2 <= g + g / 8) g = g2;

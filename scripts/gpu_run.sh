@@ -297,6 +297,16 @@ for step in "$@"; do
                 done
             done
             for f in "$OUT"/ab*_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"us_per_pivot": [0-9.]*' $f | tail -1)"; done ;;
+        selg)
+            # selection blocks on one XCD: 64 (rows / 64) against 128 at cfg3
+            for rep in 1 2; do
+                for GB in 0 128; do
+                    for B in 32 48; do
+                        LPGPU_SEL_BLOCKS=$GB run selg_${GB}_b${B}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --block $B --steps 64 --warmup 4
+                    done
+                done
+            done
+            for f in "$OUT"/selg_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"us_per_pivot": [0-9.]*' $f | tail -1)"; done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
