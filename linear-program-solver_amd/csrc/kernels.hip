@@ -2085,6 +2085,169 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
     }
 }
 
+// ---------------------------------------------------------------------------
+// K3'': k_sweep_dp with the multipliers staged through a per-wave LDS slot
+//   (k_sweep_dp2, LPGPU_SWEEP_DP=2, A/B).  A batch's 4 x NB multipliers
+//   arrive with 2 coalesced 16-byte loads per lane (lane l: pivot l's four
+//   rows, half a batch per 32 lanes) instead of NB/4 replicated 8-byte loads,
+//   are written to the slot half a batch at a time, and each 4-pivot chunk's
+//   register is read back just in time (one ds_read_b64, 16 addresses
+//   broadcast over the four 16-lane rows) -- about 80 VGPRs instead of 125,
+//   6 waves per SIMD instead of 4.  Same FMAs in the same order.
+// ---------------------------------------------------------------------------
+template <int W, int NB, int SA>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(5, 8)))
+k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
+            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
+            int nstrips, long long span)
+{
+    constexpr int RW = 4;                        // rows per batch
+    constexpr int NM = NB / 4;                   // 4-pivot chunks
+    constexpr int NH = NB / 2;                   // pivots per staged half
+    static_assert(NB % 8 == 0 && NB <= BMAX && NH <= 32, "k_sweep_dp2: pivots per sweep");
+    __shared__ double2 sp[NB][64];               // the strip's slice of P
+    __shared__ double sm[W][NH * RW];            // per wave: half a batch's multipliers, [chunk][16]
+    __shared__ long long sr[NB];
+    const int nd = (int)ctl->ndef[grp];
+    if (nd == 0 || ctl->bar_timeout) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ldb = (int)(ld * 8);
+    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
+    // lane l stages pivot h NH + (l & 31) of half h = l >> 5 (pivots past nd
+    // read pivot nd - 1's: finite, and their P is 0)
+    const int hl = lane >> 5, sl = lane & 31;
+    const bool stager = sl < NH;
+    const int sv = min(hl * NH + sl, nd - 1);
+    const int nch = (nd + 3) >> 2;
+    double *smw = &sm[wave][0];
+    // rows [r0, r1) of one strip
+    auto piece = [&](int strip, long long r0, long long r1) {
+        const long long c0 = (long long)strip * 128;
+        const int lo = min(lane * 2, (int)(ld - c0) - 2);
+        const int lob = lo * 8;
+        const double *Ts = T + c0;
+        double *Tos = Tout + c0;
+        for (int s = wave; s < NB; s += W)
+            sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
+        auto load_m = [&](double2 (&mv)[2], long long rb) {
+            const int kmax = (int)(r1 - 1 - rb);
+            const __amdgpu_buffer_rsrc_t rm = buf_rsrc(M + rb);
+            const int base = sv * (int)rows * 8;
+            if (kmax >= 3) {
+                mv[0] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rm, base, 0, 0));
+                mv[1] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rm, base + 16, 0, 0));
+            } else {   // the last batch of a piece: rows past r1 repeat row r1 - 1
+                double v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rm, base + min(k, kmax) * 8, 0, 0));
+                mv[0] = make_double2(v[0], v[1]);
+                mv[1] = make_double2(v[2], v[3]);
+            }
+        };
+        auto load_x = [&](double2 (&x)[RW], long long rb) {
+            const int kmax = (int)(r1 - 1 - rb);
+            const __amdgpu_buffer_rsrc_t rt = buf_rsrc(Ts + rb * ld);
+#pragma unroll
+            for (int k = 0; k < RW; ++k)
+                x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rt, lob, min(k, kmax) * ldb, 0));
+        };
+        // half h of the batch's multipliers into the wave's slot: chunk c, value
+        // 4 s' + k at [c * 16 + 4 s' + k] = [s * 4 + k] for the half's pivot s
+        auto stage = [&](const double2 (&mv)[2], int h) {
+            if (hl == h && stager) {
+                reinterpret_cast<double2 *>(smw)[2 * sl] = mv[0];
+                reinterpret_cast<double2 *>(smw)[2 * sl + 1] = mv[1];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        const long long step = (long long)W * RW;
+        long long rb = r0 + (long long)wave * RW;
+        double2 xn[RW], mv[2];
+        if (rb < r1) {
+            load_x(xn, rb);
+            load_m(mv, rb);
+        }
+        __syncthreads();                         // sp (and sr) staged
+        for (; rb < r1; rb += step) {
+            double2 x[RW];
+#pragma unroll
+            for (int k = 0; k < RW; ++k) x[k] = xn[k];
+            const long long rn = rb + step;
+            const bool more = rn < r1;
+            if (more) load_x(xn, rn);
+            const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
+            // a whole chunk's P (4 pivots) is read from LDS while the previous
+            // chunk's 32 FMAs run
+            double2 pc[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pc[u] = sp[u][lane];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                stage(mv, h);
+                if (h == 1 && more) load_m(mv, rn);   // the next batch's, in flight from here
+                double m = smw[lane & 15];
+#pragma unroll
+                for (int cl = 0; cl < NM / 2; ++cl) {
+                    const int c = h * (NM / 2) + cl;
+                    const double mn = smw[((cl + 1) % (NM / 2)) * 16 + (lane & 15)];
+                    double2 pn[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pn[u] = sp[(4 * c + 4 + u) % NB][lane];
+                    if (c < nch) {               // wave-uniform
+                        dp_half(x, m, pc[0], pc[1], 0);
+                        dp_half(x, m, pc[2], pc[3], 1);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pc[u] = pn[u];
+                    m = mn;
+                }
+            }
+            // a row that was pivot row s of the group: recomputed from P (rare)
+            const long long R = sr[lane % NB];
+            if (__builtin_expect(__ballot(R >= rb && R < rb + RW) != 0, 0)) {
+#pragma unroll
+                for (int k = 0; k < RW; ++k) {
+                    const long long row = rb + min(k, kmax);
+                    int sl2 = -1;
+                    for (int s = 0; s < nd; ++s)
+                        if (sr[s] == row) sl2 = s;
+                    if (sl2 >= 0) {
+                        double2 y = sp[sl2][lane];
+                        for (int s = sl2 + 1; s < nd; ++s) {
+                            const double f = M[s * rows + row];
+                            const double2 pv = sp[s][lane];
+                            y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
+                        }
+                        x[k] = y;
+                    }
+                }
+            }
+            const __amdgpu_buffer_rsrc_t ro = buf_rsrc(Tos + rb * ld);
+#pragma unroll
+            for (int k = 0; k < RW; ++k)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
+        }
+    };
+    // the (strip, row) space in strip-major order, `span` rows of it per
+    // workgroup: every workgroup of the one resident wave of them gets the
+    // same work (strip x row-run tiles left some CUs one workgroup short)
+    const long long total = (long long)nstrips * rows;
+    long long lin = (long long)blockIdx.x * span;
+    const long long lend = min(total, lin + span);
+    while (lin < lend) {
+        const int strip = (int)(lin / rows);
+        const long long r0 = lin % rows;
+        const long long r1 = min(rows, r0 + (lend - lin));
+        piece(strip, r0, r1);
+        lin += r1 - r0;
+        __syncthreads();                         // sp is restaged for the next strip
+    }
+}
+
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
 // into rank p's summary slot, then every lane waits for rank p's granule in
 // the local buffer (bounded)
@@ -2368,18 +2531,33 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
     const long long ns = (A.ld + 127) / 128;
     if (dpp) {
         const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
-        const int wv = W;
+        int wv = W;
         const void *fn = nb == 16 ? (const void *)&k_sweep_dp<W, 16, SA>
                        : nb == 32 ? (const void *)&k_sweep_dp<W, 32, SA>
                        : nb == 48 ? (const void *)&k_sweep_dp<W, 48, SA>
                                   : (const void *)&k_sweep_dp<W, 64, SA>;
+        if (dpp == 2) {
+            wv = 10;
+            fn = nb == 16 ? (const void *)&k_sweep_dp2<10, 16, SA>
+               : nb == 32 ? (const void *)&k_sweep_dp2<10, 32, SA>
+               : nb == 48 ? (const void *)&k_sweep_dp2<10, 48, SA>
+                          : (const void *)&k_sweep_dp2<10, 64, SA>;
+        }
         const int bpc = sweep_blocks_per_cu(fn, 64 * wv);
         long long nrun = (long long)sweep_cus() * bpc / ns;
         if (nrun < 1) nrun = 1;
         long long run = (A.rows + nrun - 1) / nrun;
         run = (run + RW - 1) / RW * RW;
         nrun = (A.rows + run - 1) / run;
-        const dim3 grid((unsigned)(nrun * ns));
+        dim3 grid((unsigned)(nrun * ns));
+        if (dpp == 2) {
+            // equal spans of the strip-major (strip, row) space, one per resident workgroup
+            const long long nwg = (long long)sweep_cus() * bpc;
+            long long span = (ns * A.rows + nwg - 1) / nwg;
+            span = (span + RW - 1) / RW * RW;
+            run = span;
+            grid = dim3((unsigned)((ns * A.rows + span - 1) / span));
+        }
         const Args *ap = &A;
         const double *T = ap->T, *Pp = ap->P, *Mp = ap->M;
         double *To = ap->T;

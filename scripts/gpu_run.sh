@@ -307,6 +307,23 @@ for step in "$@"; do
                 done
             done
             for f in "$OUT"/selg_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"us_per_pivot": [0-9.]*' $f | tail -1)"; done ;;
+        lite)
+            for rep in 1 2; do
+                for PL in 0 1 2; do
+                    LPGPU_POLL_LITE=$PL run lite4_${PL}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                    LPGPU_POLL_LITE=$PL run lite3_${PL}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
+                done
+            done
+            for f in "$OUT"/lite*_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"us_per_pivot": [0-9.]*' $f | tail -1)"; done ;;
+        dp2)
+            LPGPU_SWEEP_DP=2 run pytest_dp2 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_r2.py tests/test_gpu_ties.py -k "block_size or cfg3_full or cfg4 or ragged or tie" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2; do
+                for D in 1 2; do
+                    LPGPU_SWEEP_DP=$D run dp4_${D}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                    LPGPU_SWEEP_DP=$D run dp3_${D}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
+                done
+            done
+            for f in "$OUT"/dp[34]_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"avg_launch_us": [0-9.]*' $f | head -1)"; done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
