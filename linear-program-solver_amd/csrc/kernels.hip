@@ -2099,7 +2099,7 @@ template <int W, int NB, int SA>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(5, 8)))
 k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
             const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-            int nstrips, long long span)
+            int nstrips, long long run)
 {
     constexpr int RW = 4;                        // rows per batch
     constexpr int NM = NB / 4;                   // 4-pivot chunks
@@ -2232,20 +2232,14 @@ k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const d
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
         }
     };
-    // the (strip, row) space in strip-major order, `span` rows of it per
-    // workgroup: every workgroup of the one resident wave of them gets the
-    // same work (strip x row-run tiles left some CUs one workgroup short)
-    const long long total = (long long)nstrips * rows;
-    long long lin = (long long)blockIdx.x * span;
-    const long long lend = min(total, lin + span);
-    while (lin < lend) {
-        const int strip = (int)(lin / rows);
-        const long long r0 = lin % rows;
-        const long long r1 = min(rows, r0 + (lend - lin));
-        piece(strip, r0, r1);
-        lin += r1 - r0;
-        __syncthreads();                         // sp is restaged for the next strip
-    }
+    // block b: strip b % nstrips of row run b / nstrips -- consecutive blocks,
+    // dealt round-robin over the XCDs, update the same rows at the same time,
+    // so each run's multipliers are fetched about once per XCD (equal spans
+    // of the strip-major (strip, row) space instead, one per resident
+    // workgroup, re-fetched them per strip: 119 -> 174 us at cfg3)
+    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
+    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
+    piece(strip, r0, min(rows, r0 + run));
 }
 
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
@@ -2523,7 +2517,10 @@ static int sweep_blocks_per_cu(const void *fn, int threads)
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0, hipEvent_t e1)
 {
     constexpr int W = 8, RW = 4, SA = 16;
-    static int dpp = -1;    // A/B: the DPP-broadcast sweep (k_sweep_dp)
+    // LPGPU_SWEEP_DP (A/B): 1 (default) k_sweep_dp2 up to 48 pivots per sweep and
+    // k_sweep_dp at 64 (cfg3 B = 48: 119 against 126-128 us; cfg4 B = 64: 1083-1089
+    // against 1093-1096 us), 2 k_sweep_dp2 always, 3 k_sweep_dp always, 0 k_sweep_st
+    static int dpp = -1;
     if (dpp < 0) {
         const char *v = std::getenv("LPGPU_SWEEP_DP");
         dpp = v ? std::atoi(v) : 1;
@@ -2536,7 +2533,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
                        : nb == 32 ? (const void *)&k_sweep_dp<W, 32, SA>
                        : nb == 48 ? (const void *)&k_sweep_dp<W, 48, SA>
                                   : (const void *)&k_sweep_dp<W, 64, SA>;
-        if (dpp == 2) {
+        if (dpp == 2 || (dpp == 1 && nb <= 48)) {
             wv = 10;
             fn = nb == 16 ? (const void *)&k_sweep_dp2<10, 16, SA>
                : nb == 32 ? (const void *)&k_sweep_dp2<10, 32, SA>
@@ -2549,15 +2546,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         long long run = (A.rows + nrun - 1) / nrun;
         run = (run + RW - 1) / RW * RW;
         nrun = (A.rows + run - 1) / run;
-        dim3 grid((unsigned)(nrun * ns));
-        if (dpp == 2) {
-            // equal spans of the strip-major (strip, row) space, one per resident workgroup
-            const long long nwg = (long long)sweep_cus() * bpc;
-            long long span = (ns * A.rows + nwg - 1) / nwg;
-            span = (span + RW - 1) / RW * RW;
-            run = span;
-            grid = dim3((unsigned)((ns * A.rows + span - 1) / span));
-        }
+        const dim3 grid((unsigned)(nrun * ns));
         const Args *ap = &A;
         const double *T = ap->T, *Pp = ap->P, *Mp = ap->M;
         double *To = ap->T;

@@ -318,7 +318,7 @@ for step in "$@"; do
         dp2)
             LPGPU_SWEEP_DP=2 run pytest_dp2 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_r2.py tests/test_gpu_ties.py -k "block_size or cfg3_full or cfg4 or ragged or tie" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
             for rep in 1 2; do
-                for D in 1 2; do
+                for D in 1 3; do
                     LPGPU_SWEEP_DP=$D run dp4_${D}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
                     LPGPU_SWEEP_DP=$D run dp3_${D}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
                 done
