@@ -1297,7 +1297,23 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
 #pragma unroll
             for (int k = 0; k < RPL; ++k) anyp = anyp || (own[k] && ownpiv[k] != 0);
             const bool sel = __ballot(anyp) != 0;
-            for (int s0 = 0; s0 < t; s0 += CH) {
+            // whole chunks without a pivot row among the own rows: no
+            // per-pivot branch (the common case), the rest guarded
+            const int tfull = sel ? 0 : (t & ~(CH - 1));
+            for (int s0 = 0; s0 < tfull; s0 += CH) {
+                double pc[CH], mm[RPL][CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    pc[u] = sPc[s0 + u];
+#pragma unroll
+                    for (int k = 0; k < RPL; ++k) mm[k][u] = mrow[k][s0 + u];
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+#pragma unroll
+                    for (int k = 0; k < RPL; ++k) a[k] = fma(-mm[k][u], pc[u], a[k]);
+            }
+            for (int s0 = tfull; s0 < t; s0 += CH) {
                 double pc[CH], mm[RPL][CH];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
@@ -1449,7 +1465,23 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             __syncthreads();
             stamp(A, b, t, 8);
             const double av = XR ? avv : sMr[t];
-            for (int s0 = 0; s0 < t; s0 += CH) {
+            // whole chunks when row Rl was no earlier pivot row: no per-pivot
+            // branch (the common case), the rest guarded
+            const int tfull = rpiv ? 0 : (t & ~(CH - 1));
+            for (int s0 = 0; s0 < tfull; s0 += CH) {
+                double mr[CH], pv[CH][IPL];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    mr[u] = sMr[s0 + u];
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) pv[u][k] = pcol[k][s0 + u];
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) xv[k] = fma(-mr[u], pv[u][k], xv[k]);
+            }
+            for (int s0 = tfull; s0 < t; s0 += CH) {
                 double mr[CH], pv[CH][IPL];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
