@@ -2005,7 +2005,7 @@ __device__ __forceinline__ void dp_half(double2 (&x)[4], double m, double2 p0, d
 #undef DPP_PIVOT
 #undef DPF
 
-template <int W, int NB, int SA>
+template <int W, int NB, int SA, int LA = 0>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
@@ -2048,7 +2048,7 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
         const __amdgpu_buffer_rsrc_t rt = buf_rsrc(Ts + rb * ld);
 #pragma unroll
         for (int k = 0; k < RW; ++k)
-            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rt, lob, min(k, kmax) * ldb, 0));
+            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rt, lob, min(k, kmax) * ldb, LA));
     };
     const long long step = (long long)W * RW;
     long long rb = r0 + (long long)wave * RW;
@@ -2561,9 +2561,22 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
     if (dpp) {
         const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
         int wv = W;
+        // LPGPU_SWEEP_NT (A/B, off by default): tableau loads non-temporal (aux
+        // nt), 1 always, 2 when the local tableau is far beyond the 256 MB
+        // Infinity Cache.  cfg4 on one GPU: the sweep 1108-1117 -> 1062-1067 us
+        // per 64-pivot launch, but the next selection's column and row reads
+        // slowed by about as much (13.8-14.1 -> 14.3-14.9 us per pivot): 31.9k
+        // against 32.1k pivots/s, within noise (as at cfg3 in round 1)
+        static int nt_env = -1;
+        if (nt_env < 0) {
+            const char *v = std::getenv("LPGPU_SWEEP_NT");
+            nt_env = v ? std::atoi(v) : 0;
+        }
+        const bool nt = nt_env == 1 || (nt_env == 2 && (double)A.rows * (double)A.ld * 8.0 > 1e9);
         const void *fn = nb == 16 ? (const void *)&k_sweep_dp<W, 16, SA>
                        : nb == 32 ? (const void *)&k_sweep_dp<W, 32, SA>
                        : nb == 48 ? (const void *)&k_sweep_dp<W, 48, SA>
+                       : nt       ? (const void *)&k_sweep_dp<W, 64, SA, 2>
                                   : (const void *)&k_sweep_dp<W, 64, SA>;
         if (dpp == 2 || (dpp == 1 && nb <= 48)) {
             wv = 10;

@@ -357,6 +357,14 @@ static int64_t row_pitch(int64_t n)
     return p0 * 64;
 }
 
+// The kernels address the multipliers (BMAX x local rows) and a row batch
+// (a few rows x pitch) with 32-bit byte offsets.
+static bool geometry_fits(int64_t m, int64_t n, int nranks)
+{
+    const int64_t rows = (m + nranks - 1) / nranks + 1;
+    return rows * lpk::BMAX * 8 + lpk::M_PAD * 8 < (int64_t(1) << 31) && n < (int64_t(1) << 26);
+}
+
 static void init_geometry(lp_handle *h, int64_t m, int64_t n, int rank, int nranks)
 {
     h->m = m;
@@ -434,6 +442,10 @@ extern "C" int lp_create(int64_t m, int64_t n, int device, lp_handle **out)
         g_create_err = "need m > 0 and n > 0";
         return LP_BAD_ARG;
     }
+    if (!geometry_fits(m, n, 1)) {
+        g_create_err = "tableau too large for one device (at most 4194302 rows, 2^26 columns)";
+        return LP_BAD_ARG;
+    }
     lp_handle *h = new lp_handle;
     h->dev = device;
     init_geometry(h, m, n, 0, 1);
@@ -468,6 +480,10 @@ extern "C" int lp_create_sharded(int64_t m, int64_t n, int device, int rank, int
         g_create_err = "need m >= nranks > 0, n > 0 and 0 <= rank < nranks";
         return LP_BAD_ARG;
     }
+    if (!geometry_fits(m, n, nranks)) {
+        g_create_err = "row block too large for one device (at most 4194302 rows, 2^26 columns)";
+        return LP_BAD_ARG;
+    }
     lp_handle *h = new lp_handle;
     h->dev = device;
     init_geometry(h, m, n, rank, nranks);
@@ -497,6 +513,10 @@ extern "C" int lp_create_group(int64_t m, int64_t n, int device, int nshards, lp
     for (int k = 0; k < nshards; ++k) out[k] = nullptr;
     if (m <= 0 || n <= 0 || nshards <= 0 || m < nshards) {
         g_create_err = "need m >= nshards > 0 and n > 0";
+        return LP_BAD_ARG;
+    }
+    if (!geometry_fits(m, n, nshards)) {
+        g_create_err = "shard too large for one device (at most 4194302 rows, 2^26 columns)";
         return LP_BAD_ARG;
     }
     auto grp = std::make_shared<GroupComm>();
@@ -1112,6 +1132,35 @@ static int recover_timeout(const Members &M, const std::vector<Args> &A, int mod
     return LP_PIVOTED;
 }
 
+// A multi-process job's ranks decide about a timed-out cross-rank group
+// together: every rank all-gathers (timed out, the group it was in) at the end
+// of each batch.  If they all timed out in the same group, each redoes it on
+// the per-pivot kernels (recover_timeout) in lock-step.  If only some did --
+// a rank that saw every summary of the last group finished it and swept its
+// rows -- the ranks' tableaux are at different pivots and cannot be realigned:
+// every rank returns LP_DEVICE_ERROR instead of running collectives that no
+// longer pair up.  (In-process shard groups time out together: one launch.)
+static int agree_on_timeout(lp_handle *h, bool &timed_out)
+{
+    auto *rc = dynamic_cast<RcclComm *>(h->comm.get());
+    // no collective at all (peer exchange only): nothing to agree with
+    if (!rc || h->nranks < 2 || (!rc->comm && !rc->host_fn)) return LP_PIVOTED;
+    const long long mine[2] = {timed_out ? 1LL : 0LL, timed_out ? (long long)h->hctl->g_npiv : -1LL};
+    std::vector<long long> all(2 * (size_t)h->nranks);
+    CALL(rc->gather_host(h, mine, all.data(), sizeof(mine)));
+    bool any = false, same = true;
+    for (int r = 0; r < h->nranks; ++r) {
+        any = any || all[2 * r] != 0;
+        same = same && all[2 * r] == all[0] && all[2 * r + 1] == all[1];
+    }
+    if (any && !same)
+        return fail(h, LP_DEVICE_ERROR,
+                    "a cross-rank selection group timed out on some ranks only; the shards are no longer "
+                    "at the same pivot");
+    timed_out = any;
+    return LP_PIVOTED;
+}
+
 // Runs pivots until the device reports a status other than LP_PIVOTED or
 // `limit` pivots have been enqueued (limit < 0: unlimited).  Pivots are
 // enqueued in groups of `block` followed by one sweep; the host knows each
@@ -1185,6 +1234,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         CALL(sync_ctl(M));
         bool timed_out = false;
         for (lp_handle *x : M) timed_out = timed_out || x->hctl->bar_timeout != 0;
+        if (geo.g > 0 && xr) CALL(agree_on_timeout(h, timed_out));
         if (timed_out) {
             if (geo.g == 0) return fail(h, LP_DEVICE_ERROR, "exchange timed out on the per-pivot path");
             if (h->strict) return fail(h, LP_DEVICE_ERROR, "persistent selection group timed out (LPGPU_STRICT)");

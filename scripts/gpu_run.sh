@@ -324,6 +324,26 @@ for step in "$@"; do
                 done
             done
             for f in "$OUT"/dp[34]_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"avg_launch_us": [0-9.]*' $f | head -1)"; done ;;
+        swx)
+            # sweep cost breakdown: diagnostic builds with parts of the sweep removed
+            for rep in 1 2; do
+                for V in ${SWX_VARIANTS:-base swx1 swx2 swx3 swx4}; do
+                    L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/$V.so
+                    [ $V = base ] && L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/liblpgpu.so
+                    LPGPU_LIB=$L run swx4_${V}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                    LPGPU_LIB=$L run swx3_${V}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
+                done
+            done
+            for f in "$OUT"/swx*_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"avg_launch_us": [0-9.]*' $f | head -1)"; done ;;
+        nt)
+            # non-temporal tableau loads in the 64-pivot sweep (cfg4 size): parity subset, then A/B
+            run pytest_nt 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_r2.py -k "block_size or cfg3_full or cfg4 or ragged" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+            for rep in 1 2 3; do
+                for NT in 0 2; do
+                    LPGPU_SWEEP_NT=$NT run nt4_${NT}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                done
+            done
+            for f in "$OUT"/nt4_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"avg_launch_us": [0-9.]*' $f | head -1)"; done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

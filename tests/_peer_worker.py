@@ -47,8 +47,11 @@ def main():
     # ranks on the one GPU, one collective per pivot beyond (lpgpu.cpp,
     # persistent_geom) or without the peer exchange
     path, fallbacks = e.exchange_path()
-    want = _lib.PATH_PEER if mode != "host" and world <= 4 else _lib.PATH_COLLECTIVE
-    assert (path, fallbacks) == (want, 0), (rank, path, fallbacks)
+    want = _lib.PATH_PEER if mode not in ("host", "fault") and world <= 4 else _lib.PATH_COLLECTIVE
+    # "fault": rank 0's first persistent launch withholds a summary (LPGPU_FAULT);
+    # every rank times out in that group, the ranks agree on it and all redo it
+    # on the per-pivot kernels with one collective per pivot
+    assert (path, fallbacks) == (want, 1 if mode == "fault" else 0), (rank, path, fallbacks)
     b, c = e.row_begin, e.row_count
     assert np.array_equal(e.rows(0, 1), o.T[:1])
     assert np.array_equal(e.rows(1 + b, c), o.T[1 + b:1 + b + c])

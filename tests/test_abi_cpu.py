@@ -47,6 +47,9 @@ def test_create_rejects_bad_shape_without_gpu():
     assert lib.lp_create(0, 4, 0, ctypes.byref(h)) == _lib.BAD_ARG
     assert lib.lp_create(3, -1, 0, ctypes.byref(h)) == _lib.BAD_ARG
     assert b"m > 0" in lib.lp_last_error(None)
+    # 32-bit multiplier offsets: at most 4194302 rows per device
+    assert lib.lp_create(1 << 22, 4, 0, ctypes.byref(h)) == _lib.BAD_ARG
+    assert b"too large" in lib.lp_last_error(None)
 
 
 def test_no_cpu_fallback():

@@ -25,6 +25,7 @@ def _free_port():
     ("mixed", 120, 90, 20, 8, 1e-12, "scan", 2),     # + column scans, explicit pivots (host all-gather)
     ("pos", 64, 64, 10, 4, 1e-12, "scan", 2),
     ("mixed", 60, 50, 30, 8, 1e-12, "host", 2),      # every exchange through the host all-gather
+    ("mixed", 200, 150, 60, 8, 1e-12, "fault", 2),   # one rank's group times out: all ranks redo it
     # four ranks (processes sharing the one GPU)
     ("mixed", 200, 150, 60, 8, 1e-12, "peer", 4),
     ("mixed", 48, 32, 40, 4, 0.25, "peer", 4),
@@ -43,6 +44,11 @@ def test_multi_process_peer_exchange(kind, m, ns, k, block, tie, mode, world):
     for rank in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                    WORLD_SIZE=str(world), LOCAL_RANK="0")
+        if mode == "fault":
+            env.pop("LPGPU_STRICT", None)
+            env.update(LPGPU_SPIN_MAX="20000", LPGPU_XWAIT_MS="3000")
+            if rank == 0:
+                env["LPGPU_FAULT"] = "1:3"
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(HERE, "_peer_worker.py"), kind, str(m), str(ns), str(k),
              str(block), str(tie), mode], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
