@@ -46,6 +46,7 @@ from lpsol_amd import generators as gen  # noqa: E402
 
 METRIC = "pivots/sec + achieved HBM GB/s on dense float64 tableau, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+F64_PEAK_TFLOPS = 78.6      # float64 vector spec (half the guide's 157.3 TF FP32 vector)
 SWEEP_KERNEL = "k_sweep_dp"
 SEED = 3
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "hbm_traffic.json")
@@ -218,7 +219,10 @@ def accounting(steps: int, block: int, elapsed: float, sweep_avg_ms: float, sel_
     pivots = steps * block
     sweep_b = sweep_bytes(local_rows, n, block)
     achieved = sweep_b / (sweep_avg_ms * 1e-3) / 1e9 if sweep_avg_ms > 0 else 0.0
+    fma = local_rows * (n + 1) * block           # one float64 FMA per element and pivot
     return {
+        "sweep_fma_per_launch": fma,
+        "sweep_f64_TFLOPs": 2.0 * fma / (sweep_avg_ms * 1e-3) / 1e12 if sweep_avg_ms > 0 else 0.0,
         "pivots": pivots,
         "pivots_per_s": pivots / elapsed,
         "ms_per_step": 1e3 * elapsed / steps,
@@ -422,6 +426,11 @@ def main():
             "bytes_per_launch": acc["sweep_bytes_per_launch"],
             "avg_launch_us": sweep_ms * 1e3,
             "time_share": acc["sweep_time_share"],
+            # the sweep's arithmetic beside its bytes: B FMAs per element put it
+            # near the float64 ridge (78.6 TF vector spec / 8 TB/s = 9.8 flop/B)
+            "f64_fma_per_launch": acc["sweep_fma_per_launch"],
+            "f64_TFLOPs": acc["sweep_f64_TFLOPs"],
+            "f64_peak_TFLOPs": F64_PEAK_TFLOPS,
         },
         "selection": {
             "kernel": "k_group (persistent pivot selection, latency-bound)",

@@ -44,14 +44,22 @@ constexpr int SLOT_HDR = 8;        // doubles of header in front of an exchanged
 
 constexpr long long NONE = 0x7fffffffffffffffLL;
 
-// multipliers are stored pivot-major: M[s * rows + li] is the value of
-// (local row li, dC[s]) just before pivot s, so one pivot's multipliers of
-// consecutive rows are contiguous (coalesced stores, wide scalar loads)
+// multipliers: M[mi(rows, li, s)] is the value of (local row li, dC[s]) just
+// before pivot s.  Stored in 4-row quads: quad q = rows 4q..4q+3 holds its
+// BMAX pivots x 4 rows contiguously, pivot-major inside (s * 4 + row % 4).  A
+// sweep batch (4 rows, aligned) thus finds a 4-pivot chunk of its multipliers
+// in ONE 128-byte line (cfg4 sweep 1088-1100 -> 1031-1039 us per 64-pivot
+// launch against the plain pivot-major layout, scripts/sweep_probe.hip), and
+// one pivot's multipliers of 4 consecutive rows are 32 contiguous bytes.
 __host__ __device__ inline long long mi(long long rows, long long li, long long s)
 {
-    return s * rows + li;
+    (void)rows;
+    return (li >> 2) * (4LL * BMAX) + s * 4 + (li & 3);
 }
-constexpr int M_PAD = 64;          // doubles after each parity's M (wide loads past the last row)
+// doubles of one M set: whole quads (a batch's loads past the last row stay
+// inside its quad) + padding
+__host__ __device__ inline long long m_len(long long rows) { return (rows + 3) / 4 * 4 * BMAX; }
+constexpr int M_PAD = 64;          // doubles after each parity's M
 
 // Device-resident control block: the pivot loop's whole state lives here so
 // batches of pivots are enqueued without host round trips.

@@ -1858,14 +1858,14 @@ __device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)
 #pragma unroll
     for (int q = 0; q < MPL; ++q) {
         const int e = lane + 64 * q, s = e / RW;
-        mof[q] = (s < nd ? s : 0) * (int)rows;   // + min(row in batch, kmax)
+        mof[q] = (s < nd ? s : 0) * 4;           // + min(row in batch, kmax) (4-row quads, mi())
         mlive[q] = s < nd;
     }
     // rows past r1 re-load row r1 - 1 (in bounds) and are never stored
     auto load = [&](double2 (&x)[RW], double (&mv)[MPL], long long rb) {
         const int kmax = (int)(r1 - 1 - rb);
         const __amdgpu_buffer_rsrc_t rt = buf_rsrc(Ts + rb * ld);
-        const __amdgpu_buffer_rsrc_t rm = buf_rsrc(M + rb);
+        const __amdgpu_buffer_rsrc_t rm = buf_rsrc(M + (rb >> 2) * (4 * BMAX));
 #pragma unroll
         for (int q = 0; q < MPL; ++q) {
             const int k = (lane + 64 * q) % RW;
@@ -1947,6 +1947,7 @@ k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
            const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
            long long run)
 {
+    static_assert(RW == 4, "k_sweep_st: batches are the 4-row quads of M (mi())");
     static_assert(RW % 2 == 0 && NB <= BMAX && (NB * RW) % 64 == 0, "k_sweep_st: batch shape");
     __shared__ double2 sp[NB][64];              // the strip's slice of P
     __shared__ double2 sm[W][NB][RW / 2];       // per wave: the current batch's multipliers
@@ -2041,7 +2042,7 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
     auto load_m = [&](long long rb, int c) {
         const int mk = min(qk, (int)(r1 - 1 - rb));
         const int sv = min(4 * c + qs, nd - 1);
-        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(buf_rsrc(M + rb), (sv * (int)rows + mk) * 8, 0, 0));
+        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(buf_rsrc(M + (rb >> 2) * (4 * BMAX)), (sv * 4 + mk) * 8, 0, 0));
     };
     auto load_x = [&](double2 (&x)[RW], long long rb) {
         const int kmax = (int)(r1 - 1 - rb);
@@ -2102,7 +2103,7 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
                 if (sl >= 0) {
                     double2 y = sp[sl][lane];
                     for (int s = sl + 1; s < nd; ++s) {
-                        const double f = M[s * rows + row];
+                        const double f = M[mi(rows, row, s)];
                         const double2 pv = sp[s][lane];
                         y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
                     }
@@ -2164,8 +2165,8 @@ k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const d
             sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
         auto load_m = [&](double2 (&mv)[2], long long rb) {
             const int kmax = (int)(r1 - 1 - rb);
-            const __amdgpu_buffer_rsrc_t rm = buf_rsrc(M + rb);
-            const int base = sv * (int)rows * 8;
+            const __amdgpu_buffer_rsrc_t rm = buf_rsrc(M + (rb >> 2) * (4 * BMAX));
+            const int base = sv * 4 * 8;                  // pivot sv's 4 rows: 32 contiguous bytes
             if (kmax >= 3) {
                 mv[0] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rm, base, 0, 0));
                 mv[1] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rm, base + 16, 0, 0));
@@ -2250,7 +2251,7 @@ k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const d
                     if (sl2 >= 0) {
                         double2 y = sp[sl2][lane];
                         for (int s = sl2 + 1; s < nd; ++s) {
-                            const double f = M[s * rows + row];
+                            const double f = M[mi(rows, row, s)];
                             const double2 pv = sp[s][lane];
                             y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
                         }

@@ -362,7 +362,7 @@ static int64_t row_pitch(int64_t n)
 static bool geometry_fits(int64_t m, int64_t n, int nranks)
 {
     const int64_t rows = (m + nranks - 1) / nranks + 1;
-    return rows * lpk::BMAX * 8 + lpk::M_PAD * 8 < (int64_t(1) << 31) && n < (int64_t(1) << 26);
+    return (lpk::m_len(rows) + lpk::M_PAD) * 8 < (int64_t(1) << 31) && n < (int64_t(1) << 26);
 }
 
 static void init_geometry(lp_handle *h, int64_t m, int64_t n, int rank, int nranks)
@@ -400,7 +400,7 @@ static int alloc_handle(lp_handle *h)
     // two sets of group data (P, M, dR, dC) by group parity
     HCHK(h, hipMalloc(&h->P, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double)));
     HCHK(h, hipMemsetAsync(h->P, 0, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
-    const size_t mbytes = 2 * ((size_t)lpk::BMAX * h->rows + lpk::M_PAD) * sizeof(double);
+    const size_t mbytes = 2 * ((size_t)lpk::m_len(h->rows) + lpk::M_PAD) * sizeof(double);
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
     const size_t gbytes = 3 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);   // k_group summary regions

@@ -335,15 +335,13 @@ for step in "$@"; do
                 done
             done
             for f in "$OUT"/swx*_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"avg_launch_us": [0-9.]*' $f | head -1)"; done ;;
-        nt)
-            # non-temporal tableau loads in the 64-pivot sweep (cfg4 size): parity subset, then A/B
-            run pytest_nt 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_r2.py -k "block_size or cfg3_full or cfg4 or ragged" -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
-            for rep in 1 2 3; do
-                for NT in 0 2; do
-                    LPGPU_SWEEP_NT=$NT run nt4_${NT}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
-                done
+        timing)
+            # cfg4 and cfg3 timing, two runs each (auto pivots per sweep)
+            for rep in 1 2; do
+                run t4_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                run t3_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
             done
-            for f in "$OUT"/nt4_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"avg_launch_us": [0-9.]*' $f | head -1)"; done ;;
+            for f in "$OUT"/t[34]_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 2))"; done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
