@@ -45,20 +45,27 @@ constexpr int SLOT_HDR = 8;        // doubles of header in front of an exchanged
 constexpr long long NONE = 0x7fffffffffffffffLL;
 
 // multipliers: M[mi(rows, li, s)] is the value of (local row li, dC[s]) just
-// before pivot s.  Stored in 4-row quads: quad q = rows 4q..4q+3 holds its
-// BMAX pivots x 4 rows contiguously, pivot-major inside (s * 4 + row % 4).  A
-// sweep batch (4 rows, aligned) thus finds a 4-pivot chunk of its multipliers
-// in ONE 128-byte line (cfg4 sweep 1088-1100 -> 1031-1039 us per 64-pivot
-// launch against the plain pivot-major layout, scripts/sweep_probe.hip), and
-// one pivot's multipliers of 4 consecutive rows are 32 contiguous bytes.
+// before pivot s, pivot-major: one pivot's multipliers of consecutive rows are
+// contiguous (the selection stores a pivot's column with one coalesced store
+// per 64 rows).
 __host__ __device__ inline long long mi(long long rows, long long li, long long s)
 {
-    (void)rows;
+    return s * rows + li;
+}
+// The sweep's copy MQ (written by the selection at the end of each group, from
+// the multipliers it keeps in LDS): 4-row quads, quad q = rows 4q..4q+3 holds
+// its BMAX pivots x 4 rows contiguously, pivot-major inside (s * 4 + row % 4),
+// so a sweep batch (4 rows, aligned) finds a 4-pivot chunk of its multipliers
+// in ONE 128-byte line (cfg4 sweep 1106 -> 1046 us per 64-pivot launch,
+// scripts/sweep_probe.hip: 1088-1100 -> 1031-1039).  Selection stores in this
+// layout per pivot (64 rows -> 16 lines) cost 0.6 us per pivot at cfg4.
+__host__ __device__ inline long long mq(long long li, long long s)
+{
     return (li >> 2) * (4LL * BMAX) + s * 4 + (li & 3);
 }
-// doubles of one M set: whole quads (a batch's loads past the last row stay
-// inside its quad) + padding
-__host__ __device__ inline long long m_len(long long rows) { return (rows + 3) / 4 * 4 * BMAX; }
+// doubles of MQ: whole quads (a batch's loads past the last row stay inside
+// its quad)
+__host__ __device__ inline long long mq_len(long long rows) { return (rows + 3) / 4 * 4 * BMAX; }
 constexpr int M_PAD = 64;          // doubles after each parity's M
 
 // Device-resident control block: the pivot loop's whole state lives here so
@@ -119,6 +126,7 @@ struct Args {
     double *row0;        // current row 0 (ld doubles)
     double *col0;        // current column 0 of the local rows (rows doubles)
     double *M;           // BMAX x rows multipliers, pivot-major (mi())
+    double *MQ;          // the sweep's copy of M in 4-row quads (mq())
     double *P;           // BMAX x ld normalised pivot rows
     long long *dR;       // BMAX local pivot rows (-1: another rank's row)
     long long *dC;       // BMAX pivot columns (tableau index)

@@ -440,7 +440,10 @@ k_ratio(Args A, int t, int grp, int mode, int from_erec, long long check_row)
         sR[threadIdx.x] = A.dR[threadIdx.x];
         sPc[threadIdx.x] = A.P[threadIdx.x * A.ld + C];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) A.M[mi(A.rows, 0, t)] = A.row0[C];   // row 0's multiplier
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // row 0's multiplier (+ the sweep's copy)
+        A.M[mi(A.rows, 0, t)] = A.row0[C];
+        A.MQ[mq(0, t)] = A.row0[C];
+    }
     __syncthreads();
 
     const long long li0 = 1 + (long long)blockIdx.x * RATIO_CHUNK;
@@ -451,6 +454,7 @@ k_ratio(Args A, int t, int grp, int mode, int from_erec, long long check_row)
     if (li < li1) {
         const double a = current_col<TP>(A, t, li, A.T[li * A.ld + C], sR, sPc);
         A.M[mi(A.rows, li, t)] = a;
+        A.MQ[mq(li, t)] = a;
         q = row_ratio(a, A.col0[li], A.tol, ok);
     }
     const double lb = block_min(ok ? q : INFINITY, sd);
@@ -562,8 +566,11 @@ __global__ void k_gather(Args A, int t)
     if (ctl->status != LP_PIVOTED) return;
     const long long C = ctl->c + 1;
     for (long long li = blockIdx.x * (long long)blockDim.x + threadIdx.x; li < A.rows;
-         li += (long long)gridDim.x * blockDim.x)
-        A.M[mi(A.rows, li, t)] = li == 0 ? A.row0[C] : current(A, t, li, C, A.T[li * A.ld + C]);
+         li += (long long)gridDim.x * blockDim.x) {
+        const double mv = li == 0 ? A.row0[C] : current(A, t, li, C, A.T[li * A.ld + C]);
+        A.M[mi(A.rows, li, t)] = mv;
+        A.MQ[mq(li, t)] = mv;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1147,6 +1154,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
 #pragma unroll
     for (int k = 0; k < RPL; ++k) ownpiv[k] = 0;
     int stop = 0;                     // block 0: the objective increased (simplex.py:133)
+    int ndone = 0;                    // pivots of this launch completed (their M in lM)
     for (int tv = 0; tv < count; ++tv) {
         // the pivot index is wave-uniform; saying so keeps the chains'
         // trip counts and bounds in SGPRs (scalar branches, no exec masking:
@@ -1281,7 +1289,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         if (tid < t) sPc[tid] = ld_sc1(&A.P[tid * A.ld + C]);
         if (tid == 0) {
             if (b == 0) st_x(&ctl->c, C - 1, fast);
-            if (C >= jc0 && C < jc1) st_x(&A.M[mi(A.rows, 0, t)], l0[C - jc0], fast);   // row 0's multiplier
+            if (C >= jc0 && C < jc1) {   // row 0's multiplier (+ the sweep's copy, read after the launch)
+                st_x(&A.M[mi(A.rows, 0, t)], l0[C - jc0], fast);
+                *gp(&A.MQ[mq(0, t)]) = l0[C - jc0];
+            }
         }
         __syncthreads();
         stamp(A, b, t, 3);
@@ -1773,6 +1784,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         }
         bstamp(A, b, t, 1);
         ++npiv;
+        ++ndone;
         stamp(A, b, t, 11);
         pending = t;
         pendR = R;
@@ -1789,6 +1801,20 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 if (own[k]) st_x(&A.col0[li[k]], upd(li[k], pendR, mrow[k][pending], pl, lc[tid + k * nth]), fast);
         } else {
             status = LP_DEVICE_ERROR;
+        }
+    }
+    // the sweep's copy of the group's multipliers of the own rows (MQ, 4-row
+    // quads) from LDS: consecutive lanes store consecutive doubles of the
+    // block's quads (the quads shared with a neighbour block: own rows only);
+    // read after the launch, so plain stores (issued before the last
+    // exchange's wait instead: 0.1 us per pivot slower)
+    {
+        const int nds = __builtin_amdgcn_readfirstlane(ndone);
+        const long long e0 = (lr0 >> 2) * (4 * BMAX), e1 = (((lr1 - 1) >> 2) + 1) * (4 * BMAX);
+        for (long long e = e0 + tid; e < e1 && nds > 0; e += nth) {
+            const long long row = e / (4 * BMAX) * 4 + (e & 3);
+            const int s = (int)(e % (4 * BMAX) >> 2);
+            if (row >= lr0 && row < lr1 && s < nds) *gp(&A.MQ[e]) = lM[(row - lr0) * cs + s];
         }
     }
     if (b == 0 && tid == 0) {
@@ -2103,7 +2129,7 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
                 if (sl >= 0) {
                     double2 y = sp[sl][lane];
                     for (int s = sl + 1; s < nd; ++s) {
-                        const double f = M[mi(rows, row, s)];
+                        const double f = M[mq(row, s)];
                         const double2 pv = sp[s][lane];
                         y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
                     }
@@ -2251,7 +2277,7 @@ k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const d
                     if (sl2 >= 0) {
                         double2 y = sp[sl2][lane];
                         for (int s = sl2 + 1; s < nd; ++s) {
-                            const double f = M[mi(rows, row, s)];
+                            const double f = M[mq(row, s)];
                             const double2 pv = sp[s][lane];
                             y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
                         }
@@ -2594,7 +2620,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         nrun = (A.rows + run - 1) / run;
         const dim3 grid((unsigned)(nrun * ns));
         const Args *ap = &A;
-        const double *T = ap->T, *Pp = ap->P, *Mp = ap->M;
+        const double *T = ap->T, *Pp = ap->P, *Mp = ap->MQ;   // the sweep reads the quad copy
         double *To = ap->T;
         const long long *dRp = ap->dR;
         const Ctl *ctlp = ap->ctl;
@@ -2613,7 +2639,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
     const dim3 grid((unsigned)(nrun * ns));
 #define SWEEP_ST_ONE(NBV)                                                                            \
     hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, 0, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, A.T, \
-                          A.P, A.M, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
+                          A.P, A.MQ, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
     if (nd_max <= 16) SWEEP_ST_ONE(16);
     else if (nd_max <= 32) SWEEP_ST_ONE(32);
     else if (nd_max <= 48) SWEEP_ST_ONE(48);

@@ -39,7 +39,7 @@ struct lp_handle {
     int64_t m = 0, n = 0, ld = 0;   // global problem
     int64_t rb = 0, rc = 0;         // local constraint block [rb, rb+rc)
     int64_t rows = 0;               // local rows = rc + 1
-    double *T = nullptr, *P = nullptr, *M = nullptr, *row0 = nullptr, *col0 = nullptr;
+    double *T = nullptr, *P = nullptr, *M = nullptr, *MQ = nullptr, *row0 = nullptr, *col0 = nullptr;
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
     int block = 0;                  // pivots deferred into one sweep (1..BMAX; 0 = auto)
@@ -273,6 +273,7 @@ static Args args_of(const lp_handle *h)
     A.row0 = h->row0;
     A.col0 = h->col0;
     A.M = h->M;
+    A.MQ = h->MQ;
     A.P = h->P;
     A.dR = h->dR;
     A.dC = h->dC;
@@ -362,7 +363,7 @@ static int64_t row_pitch(int64_t n)
 static bool geometry_fits(int64_t m, int64_t n, int nranks)
 {
     const int64_t rows = (m + nranks - 1) / nranks + 1;
-    return (lpk::m_len(rows) + lpk::M_PAD) * 8 < (int64_t(1) << 31) && n < (int64_t(1) << 26);
+    return (rows * lpk::BMAX + lpk::M_PAD) * 8 < (int64_t(1) << 31) && n < (int64_t(1) << 26);
 }
 
 static void init_geometry(lp_handle *h, int64_t m, int64_t n, int rank, int nranks)
@@ -400,7 +401,10 @@ static int alloc_handle(lp_handle *h)
     // two sets of group data (P, M, dR, dC) by group parity
     HCHK(h, hipMalloc(&h->P, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double)));
     HCHK(h, hipMemsetAsync(h->P, 0, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
-    const size_t mbytes = 2 * ((size_t)lpk::m_len(h->rows) + lpk::M_PAD) * sizeof(double);
+    const size_t mbytes = 2 * ((size_t)lpk::BMAX * h->rows + lpk::M_PAD) * sizeof(double);
+    const size_t mqbytes = ((size_t)lpk::mq_len(h->rows) + lpk::M_PAD) * sizeof(double);
+    HCHK(h, hipMalloc(&h->MQ, mqbytes));
+    HCHK(h, hipMemsetAsync(h->MQ, 0, mqbytes, h->s));
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
     const size_t gbytes = 3 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);   // k_group summary regions
@@ -714,6 +718,7 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->T) (void)hipFree(h->T);
     if (h->P) (void)hipFree(h->P);
     if (h->M) (void)hipFree(h->M);
+    if (h->MQ) (void)hipFree(h->MQ);
     if (h->row0) (void)hipFree(h->row0);
     if (h->col0) (void)hipFree(h->col0);
     if (h->dR) (void)hipFree(h->dR);
