@@ -84,6 +84,12 @@ def lib_digest() -> str:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def sweep_kernel(block: int) -> str:
+    """the sweep kernel the engine launches for `block` pivots per sweep
+    (kernels.hip launch_sweep: k_sweep_dp2 up to 48, k_sweep_dp at 64)"""
+    return "k_sweep_dp2" if block <= 48 else "k_sweep_dp"
+
+
 def load_traffic(path: str | None, block: int, workload_name: str, digest: str):
     """HBM bytes per sweep launch measured by scripts/hbm_traffic.py (two
     rocprofv3 --pmc passes of this bench), if measured on this very library
@@ -94,7 +100,7 @@ def load_traffic(path: str | None, block: int, workload_name: str, digest: str):
         for e in d.get("entries", [d]):
             if (e.get("block") == block and e.get("workload") == workload_name
                     and e.get("lib_sha256") == digest
-                    and e.get("kernel", "").split("<")[0] == SWEEP_KERNEL):
+                    and SWEEP_KERNEL in e.get("kernel", "")):
                 return e.get("hbm_bytes_per_launch")
     return None
 
@@ -413,7 +419,7 @@ def main():
         # immediate-update engine would need for this rate
         "unblocked_equivalent_GBps": pivot_bytes(m, n) * elapsed_pps / 1e9,
         "roofline": {
-            "kernel": f"{SWEEP_KERNEL} (rank-{B} elimination of {local_rows} local rows)",
+            "kernel": f"{sweep_kernel(B)} (rank-{B} elimination of {local_rows} local rows)",
             "bound": "hbm",
             "achieved": acc["achieved_GBps"],
             "peak": HBM_PEAK_GBPS,
@@ -448,7 +454,8 @@ def main():
             "workload": WORKLOADS["cfg3"][3], "value": c3["pivots_per_s"], "unit": "pivots/s",
             "ms_per_step": c3["ms_per_step"], "us_per_pivot": 1e6 / c3["pivots_per_s"],
             "pivots_per_step": c3["block"],
-            "roofline": {"kernel": f"{SWEEP_KERNEL} (rank-{c3['block']} elimination of 4097 rows)", "bound": "hbm",
+            "roofline": {"kernel": f"{sweep_kernel(c3['block'])} (rank-{c3['block']} elimination of 4097 rows)",
+                         "bound": "hbm",
                          "achieved": c3["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": c3["achieved_GBps"] / HBM_PEAK_GBPS,
                          "traffic": load_traffic(args.traffic_json, c3["block"], "cfg3", digest),

@@ -342,6 +342,7 @@ for step in "$@"; do
                 run t3_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4
             done
             for f in "$OUT"/t[34]_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 2))"; done ;;
+        configs) run configs 600 python bench.py --configs ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -22,6 +22,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+NAMES: set[str] = set()   # the matching kernels' names (demangled by rocprofv3)
+
+
 def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -32,6 +35,7 @@ def per_dispatch(d: str, counter: str, kernel: str) -> list[float]:
             for row in csv.DictReader(fh):
                 if kernel not in row.get("Kernel_Name", ""):
                     continue
+                NAMES.add(row["Kernel_Name"].split("(")[0])
                 if row.get("Counter_Name") != counter:
                     continue
                 key = f + ":" + row.get("Dispatch_Id", str(len(vals)))
@@ -58,7 +62,7 @@ def main():
     _, m, _, n, _, _ = bench.workload(a.workload, 1, 0)
     alg = bench.sweep_bytes(m + 1, n, a.block)
     out = {
-        "kernel": f"{a.kernel}<{a.block}>",
+        "kernel": " / ".join(sorted(NAMES)) or f"{a.kernel}<{a.block}>",
         "workload": a.workload,
         "workload_desc": bench.WORKLOADS[a.workload][3] + " (bench.py, 1 GPU)",
         "lib_sha256": bench.lib_digest(),
