@@ -79,9 +79,26 @@ def workload(name: str, nranks: int, rank: int):
     return kind, m, ns, n, m * rank // nranks, m * (rank + 1) // nranks
 
 
+SRC_FILES = [os.path.join(ROOT, "linear-program-solver_amd", "csrc", f)
+             for f in ("kernels.hip", "lpgpu.cpp", "engine.h", "Makefile")] + [
+    os.path.join(ROOT, "include", "lpgpu.h")]
+
+
 def lib_digest() -> str:
+    """sha256 of the loaded library file (reported; hipcc output is not
+    byte-reproducible, so the traffic stamp uses src_digest)"""
     with open(_lib.LIB_PATH, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def src_digest() -> str:
+    """sha256 over the library's sources and build flags: the identity of a
+    build for the PMC traffic stamp (the same sources give the same kernels)"""
+    h = hashlib.sha256()
+    for p in SRC_FILES:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def sweep_kernel(block: int) -> str:
@@ -99,7 +116,7 @@ def load_traffic(path: str | None, block: int, workload_name: str, digest: str):
             d = json.load(f)
         for e in d.get("entries", [d]):
             if (e.get("block") == block and e.get("workload") == workload_name
-                    and e.get("lib_sha256") == digest
+                    and e.get("src_sha256") == digest
                     and SWEEP_KERNEL in e.get("kernel", "")):
                 return e.get("hbm_bytes_per_launch")
     return None
@@ -330,7 +347,7 @@ def main():
     ndev = _lib.device_count()
     device = local % ndev if ndev else local     # one rank per GPU; wraps only on smaller boxes
     B = args.block
-    digest = lib_digest()
+    digest = src_digest()
     kind, m, ns, n, rb, re_ = workload(args.workload, world, rank)
     out = {"metric": METRIC, "unit": "pivots/s"}
 
@@ -426,9 +443,9 @@ def main():
             "unit": "GB/s",
             "frac": acc["achieved_GBps"] / HBM_PEAK_GBPS,
             "traffic": traffic,
-            "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch, measured on this library "
-                             "build (profiles/r02/hbm_traffic.json)" if traffic else
-                             "not measured on this library build / workload"),
+            "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch, measured on a build of these "
+                             "sources (profiles/r02/hbm_traffic.json, src_sha256)" if traffic else
+                             "not measured on a build of these sources / this workload"),
             "bytes_per_launch": acc["sweep_bytes_per_launch"],
             "avg_launch_us": sweep_ms * 1e3,
             "time_share": acc["sweep_time_share"],
@@ -446,7 +463,8 @@ def main():
             "time_share": acc["selection_time_share"],
         },
         "fallbacks": acc["fallbacks"],
-        "lib_sha256": digest,
+        "src_sha256": digest,
+        "lib_sha256": lib_digest(),
     })
     if world == 1 and args.workload != "cfg3" and not args.no_cfg3 and not args.group_shards:
         c3 = single_gpu_leg("cfg3", args.steps, args.warmup, args.block, args.profile_every, device)

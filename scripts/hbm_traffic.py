@@ -7,8 +7,9 @@ wide coalesced streaming read, so it is doubled (MI355X_MICROARCH.md §HBM).
 
 usage: python scripts/hbm_traffic.py FETCH_DIR WRITE_DIR OUT_JSON --block B --workload W
 
-The result is stamped with the sha256 of the library build that ran (bench.py
-reports it as roofline.traffic only for that build, workload and block).
+The result is stamped with the sha256 of the library's sources (bench.py
+reports it as roofline.traffic only for builds of those sources, that
+workload and block; hipcc output is not byte-reproducible, so not the .so's).
 """
 import argparse
 import csv
@@ -65,6 +66,7 @@ def main():
         "kernel": " / ".join(sorted(NAMES)) or f"{a.kernel}<{a.block}>",
         "workload": a.workload,
         "workload_desc": bench.WORKLOADS[a.workload][3] + " (bench.py, 1 GPU)",
+        "src_sha256": bench.src_digest(),
         "lib_sha256": bench.lib_digest(),
         "block": a.block,
         "dispatches": [len(fetch), len(write)],
@@ -80,8 +82,8 @@ def main():
     if os.path.exists(a.out):
         with open(a.out) as fh:
             entries = json.load(fh).get("entries", [])
-    entries = [e for e in entries if (e.get("workload"), e.get("block"), e.get("lib_sha256")) !=
-               (out["workload"], out["block"], out["lib_sha256"])] + [out]
+    entries = [e for e in entries if (e.get("workload"), e.get("block"), e.get("src_sha256")) !=
+               (out["workload"], out["block"], out["src_sha256"])] + [out]
     with open(a.out, "w") as fh:
         json.dump({"entries": entries}, fh, indent=1)
     print(json.dumps(out))

@@ -55,10 +55,10 @@ def test_accounting_per_launch(steps, block):
 
 
 def test_traffic_needs_this_build(tmp_path):
-    """roofline.traffic is reported only for the library build, workload and
+    """roofline.traffic is reported only for builds of the sources, workload and
     block the PMC passes measured (scripts/hbm_traffic.py stamps them)"""
     p = tmp_path / "t.json"
-    d = {"kernel": "k_sweep_dp<8, 32, 16, 1>", "block": 32, "workload": "cfg4", "lib_sha256": "abc",
+    d = {"kernel": "k_sweep_dp<8, 32, 16, 1>", "block": 32, "workload": "cfg4", "src_sha256": "abc",
          "hbm_bytes_per_launch": 123.0}
     p.write_text(json.dumps(d))
     assert bench.load_traffic(str(p), 32, "cfg4", "abc") == 123.0
