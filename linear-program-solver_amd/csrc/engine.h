@@ -151,7 +151,7 @@ struct Args {
     unsigned spin_max;   // k_group: polls of one exchange before it gives up (timeout)
     unsigned xwait_ms;   // k_group (XR): wall-clock bound of a cross-rank wait
     int fault;           // tests only (LPGPU_FAULT): t + 1 -> block 1 withholds pivot t's ratio summary
-    int pad1;
+    int hier;            // k_group: two-level exchange when the blocks are spread over the XCDs (1) or flat (0)
     int rank;            // this rank (row-sharded jobs)
     // row-sharded persistent selection: this rank's exchange buffer and every
     // rank's (peer[rank] == xbuf), written by the peers over xGMI
@@ -211,6 +211,7 @@ struct GroupGeom {
     int ipl = 2;         // own columns per lane (cpb <= 64 ipl)
     int rpl = 1;         // own rows per lane (rpb <= 64 rpl)
     int xmode = 0;       // 1: every block on ONE XCD (grid 8 g, blocks 0, 8, 16, ...)
+    int hk = 0;          // 1: blocks spread over the XCDs, the k_group variant with the two-level exchange
     size_t lds = 0;      // dynamic LDS per block
     int per_cu = 0;      // resident blocks per CU the launch relies on
 };

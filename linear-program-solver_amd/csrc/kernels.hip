@@ -963,6 +963,52 @@ __device__ bool gather_x(const u64 *slots, int n, unsigned tag, unsigned (&w)[NG
     }
 }
 
+// Two-level exchange, level 1 -> 2 (k_group, blocks spread over the XCDs):
+// the first block of XCD group x gathers the group's G8 summaries (logical
+// slots x G8 .. x G8 + G8 - 1, granule-major, L2-resident) and publishes ONE
+// summary of the same format to slot x of the level-2 region (block-major,
+// write-through): l = the group minimum; q, i = the candidate of the group's
+// first member within the band of l, or q = INFINITY (rescan the group) when
+// that member's own candidate lies outside it.  Entering summaries (row 0)
+// also carry fneg = the group's first column with c_j < -cost, and member 0's
+// flag bits and words 6, 7 (block 0's rule / stop flag / P[t][0] travel in
+// group 0's summary).
+template <int NG>
+__device__ bool hier_combine(const u64 *lvl1, u64 *lvl2, unsigned x, unsigned G8, unsigned tag, double tie,
+                             bool entering, unsigned *tflag, unsigned spin_max)
+{
+    unsigned w[1][NG];
+    if (!gather<1, NG>(lvl1 + x * G8, G8, tag, w, tflag, spin_max)) return false;
+    const bool in = threadIdx.x < G8;
+    const double l = in ? mk_d(w[0][0], w[0][1]) : INFINITY;
+    const double lx = wave_min(l);
+    unsigned o[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) o[g] = rl32(w[0][g], 0);   // member 0's words
+    o[0] = lo32(lx);
+    o[1] = hi32(lx);
+    if (lx < INFINITY) {
+        const double thr = tie_band(lx, tie);
+        const int f = __builtin_ctzll(__ballot(in && l <= thr));
+        double q = rl_d(w[0][2], w[0][3], f);
+        const unsigned i = rl32(w[0][4], f);
+        if (!(q <= thr)) q = INFINITY;
+        o[2] = lo32(q);
+        o[3] = hi32(q);
+        o[4] = entering ? (i & 0x7fffffffu) | (o[4] & 0x80000000u) : i;
+    }
+    if (entering) {
+        const long long fn = in ? (long long)(w[0][5] & 0x7fffffffu) : 0x7fffffffLL;
+        o[5] = (unsigned)wave_min_ll(fn) | (o[5] & 0x80000000u);
+    }
+    unsigned wv = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+        if ((int)threadIdx.x == g) wv = o[g];
+    publish(lvl2, x, tag, wv, NG, false, 1);
+    return true;
+}
+
 // row-0 summary of a block's own columns from per-lane values (columns
 // j = jc0 + lane + 64k; vv = INFINITY where j is not a variable column):
 // slice minimum el, first column within the tie band of el (ei, its value
@@ -1001,7 +1047,7 @@ __device__ __forceinline__ void row0_summary(const double (&vv)[IPL], double vmi
 // rule, cap = fmode, frule, fcap; k_reset's work), bit 1 loads the eager row 0
 // / column 0 from the stored tableau (k_load_eager's), bit 2 picks the first
 // entering column from the row-0 slices with one extra exchange (k_enter's).
-template <int NR, int IPL, int RPL, bool XR>
+template <int NR, int IPL, int RPL, bool XR, bool HK = false>
 __global__ void __launch_bounds__(GROUP_THREADS)
 k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, unsigned seq, int bmax,
         int xmode, int first, int fmode, int frule, long long fcap)
@@ -1082,10 +1128,62 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         // the compiler wait for the stores before the next one)
         fast = __builtin_amdgcn_readfirstlane(__all(same) ? 1 : 0) != 0;
     }
+    // Two-level exchange for blocks spread over the 8 XCDs (single device): the
+    // G / 8 blocks of one XCD (b % 8 equal under the round-robin dealing,
+    // checked here) exchange their summaries through that XCD's L2 (level 1,
+    // plain stores, granule-major), the XCD's first block combines them into
+    // one summary of the same format and publishes it write-through (level 2),
+    // and every block polls the 8 level-2 summaries -- instead of every block
+    // polling all G summaries across the XCDs.  Blocks are numbered XCD-major
+    // (logical L: rows and columns in L order), so the first summary within
+    // the band is found group first, then member: a group's summary carries
+    // its first member within ITS band, which is the answer whenever that
+    // candidate is inside the global band (every earlier row is above it);
+    // otherwise (q = INFINITY: a rescan) the group's rows / columns are
+    // rescanned against the global band, as a block's are in the flat form.
+    bool hier = false;
+    const unsigned G8 = G / 8;
+    // (HK: the variant compiled with it, launched for spread single-device groups)
+    if (HK && !XR && !As && !xmode && A.hier && G % 8 == 0 && G8 >= 8 && G8 <= (unsigned)GROUP_THREADS) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        u64 *grX = A.gran + 2 * GROUP_MAXBLOCKS * GSLOT;
+        if (threadIdx.x == 0) st_sc1(&grX[gslot(0, b, 0)], ((u64)gtag(seq, 0, 7) << 32) | xcc);
+        unsigned wx[NRMAX][1];
+        if (!gather<NRMAX, 1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
+            if (b == 0 && threadIdx.x == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
+            return;
+        }
+        // block l + 64k shares an XCD with block (l + 64k) % 8 (lane l % 8 of k = 0)
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < NRMAX; ++k) {
+            const unsigned x0 = (unsigned)__shfl((int)wx[0][0], (int)(threadIdx.x & 7));
+            if (threadIdx.x + k * GROUP_THREADS < G) same = same && wx[k][0] == x0;
+        }
+        hier = __builtin_amdgcn_readfirstlane(__all(same) ? 1 : 0) != 0;
+    }
+    const unsigned L = hier ? (b % 8) * G8 + b / 8 : b;     // logical block: rows, columns, flat slots
+    const unsigned Geff = hier ? 8u : G;                    // summaries in the final combine
     const long long rpb = (A.rc + G - 1) / G;               // rows per block (<= RPL nth)
-    const long long lr0 = 1 + b * rpb, lr1 = min(lr0 + rpb, A.rows);
+    const long long lr0 = 1 + L * rpb, lr1 = min(lr0 + rpb, A.rows);
     const long long cpb = (A.ld + G - 1) / G;               // columns per block (<= IPL nth)
-    const long long jc0 = b * cpb, jc1 = min(jc0 + cpb, A.ld);
+    const long long jc0 = L * cpb, jc1 = min(jc0 + cpb, A.ld);
+    const long long smul = hier ? (long long)G8 : 1;        // blocks per final summary (rescans)
+    u64 *grR2 = A.gran + 3 * GROUP_MAXBLOCKS * GSLOT;       // level 2: 8 slots x 8 granules, block-major
+    u64 *grE2 = grR2 + 8 * GSLOT;
+    // publication of a block's summary (+ the level-1 combine by an XCD's
+    // first block) and the wait for the summaries to combine
+    auto pub2 = [&](u64 *g1, u64 *g2, unsigned tag, unsigned wv, int n, double tie, bool entering) -> bool {
+        if (!hier) {
+            publish(g1, L, tag, wv, n, fast, xs);
+            return true;
+        }
+        publish(g1, L, tag, wv, n, true, 0);
+        if (b / 8 != 0) return true;
+        return entering ? hier_combine<NGE>(g1, g2, b % 8, G8, tag, tie, true, &ctl->bar_timeout, A.spin_max)
+                        : hier_combine<NGR>(g1, g2, b % 8, G8, tag, tie, false, &ctl->bar_timeout, A.spin_max);
+    };
     const int cs = bmax + 1;
     double *lM = dyn;                        // [rpb][cs]  M[own row][s]
     double *lP = lM + rpb * cs;              // [cpb][cs]  P[s][own column]
@@ -1214,10 +1312,14 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     else if (tid == 3) wv = hi32(seq_);
                     else if (tid == 4) wv = idx32(sei_);
                     else if (tid == 5) wv = idx32(sfn_) & 0x7fffffffu;
-                    publish(grE, b, etag, wv, NGE, fast, xs);
+                    if (!pub2(grE, grE2, etag, wv, NGE, A.tol.cost_tie, true)) {
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
                 }
                 unsigned w[NR][NGE];
-                if (!gather<NR, NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max, xs)) {
+                if (!(hier ? gather<NR, NGE, false>(grE2, 8, etag, w, &ctl->bar_timeout, A.spin_max)
+                           : gather<NR, NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max, xs))) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -1227,7 +1329,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     el[k] = INFINITY;
                     eq[k] = 0.0;
                     ei[k] = NONE;
-                    if (bb < G) {
+                    if (bb < Geff) {
                         el[k] = mk_d(w[k][0], w[k][1]);
                         eq[k] = mk_d(w[k][2], w[k][3]);
                         ei[k] = un_idx(w[k][4] & 0x7fffffffu);
@@ -1255,11 +1357,15 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                     C = NONE;
                 } else {
                     const double ethr = tie_band(g, A.tol.cost_tie);
-                    C = combine_loaded(el, ei, eq, G, ethr);
+                    // the summaries combined: every block's (previous launch's
+                    // records) or, two-level, the 8 XCD groups'
+                    const bool rec = t == 0 && from_erec;
+                    C = combine_loaded(el, ei, eq, rec ? G : Geff, ethr);
                     if (C < 0) {   // rare: rescan that slice of row 0
-                        const long long k0 = (-1 - C) * cpb;
+                        const long long wsl = cpb * (rec ? 1 : smul);
+                        const long long k0 = (-1 - C) * wsl;
                         long long best = NONE;
-                        for (long long k = k0 + tid; k < k0 + cpb; k += nth)
+                        for (long long k = k0 + tid; k < k0 + wsl; k += nth)
                             if (k >= 1 && k <= A.n && ld_sc1(&A.row0[k]) <= ethr) { best = k; break; }
                         C = block_min_ll(best, sl);
                     }
@@ -1394,7 +1500,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 3) wv = hi32(qb);
             else if (tid == 5) wv = lo32(ab);
             else if (tid == 6) wv = hi32(ab);
-            publish(grR, b, gtag(seq, t, 0), wv, NGRX, fast, xs);
+            if (!pub2(grR, grR2, gtag(seq, t, 0), wv, NGRX, A.tol.ratio_tie, false)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
         }
         bstamp(A, b, t, 0);
         stamp(A, b, t, 5);
@@ -1403,7 +1512,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         double rl[NR];
         double rmin = INFINITY;
         unsigned w[NR][NGRX];
-        if (!gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max, xs)) {
+        if (!(hier ? gather<NR, NGRX, false>(grR2, 8, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max)
+                   : gather<NR, NGRX>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max, xs))) {
             status = LP_DEVICE_ERROR;
             break;
         }
@@ -1411,7 +1521,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         for (int k = 0; k < NR; ++k) {
             const unsigned bb = tid + k * nth;
             rl[k] = INFINITY;
-            if (bb < G) {
+            if (bb < Geff) {
                 rl[k] = mk_d(w[k][0], w[k][1]);
                 rmin = fmin(rmin, rl[k]);
             }
@@ -1422,7 +1532,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
         double qR = 0.0, aR = 0.0;    // its ratio and pivot element (XR)
         if (g < INFINITY) {
             const double thr = tie_band(g, A.tol.ratio_tie);
-            const int bs = first_in_band(rl, G, thr);
+            const int bs = first_in_band(rl, Geff, thr);
             const int k = bs / nth, f = bs % nth;
             double q = 0.0, av_ = 0.0;
             unsigned wi = 0;
@@ -1437,8 +1547,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 R = un_idx(wi);
                 qR = q;
                 aR = av_;
-            } else {   // rare: rescan the selected block's rows (their M[t], col0 are published)
-                const long long r0 = 1 + (long long)bs * rpb, r1 = min(r0 + rpb, A.rows);
+            } else {   // rare: rescan the selected block's (group's) rows (their M[t], col0 are published)
+                const long long r0 = 1 + (long long)bs * rpb * smul, r1 = min(r0 + rpb * smul, A.rows);
                 long long mine = NONE;
                 double qm = 0.0, am = 0.0;
                 for (long long lj = r0 + tid; lj < r1; lj += nth) {
@@ -1754,7 +1864,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             else if (tid == 5) wv = (idx32(efn) & 0x7fffffffu) | ((unsigned)rule << 31);
             else if (tid == 6) wv = lo32(p0n);
             else if (tid == 7) wv = hi32(p0n);
-            publish(grE, b, gtag(seq, t, 1), wv, NGE, fast, xs);
+            if (!pub2(grE, grE2, gtag(seq, t, 1), wv, NGE, A.tol.cost_tie, true)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
         }
         // records read after the launch only (host, sweep, next launch): one
         // store instruction of the last block (block 0 already carries the
@@ -1776,10 +1889,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             st_x(&ctl->rule, (int)rule, fast);
         }
         if (t == count - 1 && tid == 0) {     // the next launch reads plain summaries
-            st_x(&A.erec[b].l, el, fast);
-            st_x(&A.erec[b].i, ei, fast);
-            st_x(&A.erec[b].q, eq, fast);
-            st_x(&A.erec[b].fneg, efn, fast);
+            st_x(&A.erec[L].l, el, fast);
+            st_x(&A.erec[L].i, ei, fast);
+            st_x(&A.erec[L].q, eq, fast);
+            st_x(&A.erec[L].fneg, efn, fast);
             if (b == 0) st_x(&A.erec[0].rule, (long long)rule, fast);
         }
         bstamp(A, b, t, 1);
@@ -1793,7 +1906,8 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     // row-0 summary
     if (pending >= 0) {
         unsigned w[NR][NGE];
-        if (gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout, A.spin_max, xs)) {
+        if (hier ? gather<NR, NGE, false>(grE2, 8, gtag(seq, pending, 1), w, &ctl->bar_timeout, A.spin_max)
+                 : gather<NR, NGE>(grE, G, gtag(seq, pending, 1), w, &ctl->bar_timeout, A.spin_max, xs)) {
             const double pl = mk_d(__builtin_amdgcn_readfirstlane(w[0][6]),
                                    __builtin_amdgcn_readfirstlane(w[0][7]));
 #pragma unroll
@@ -2653,11 +2767,12 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
 #define GROUP_VARIANTS(X) \
     X(1, 2, 1) X(2, 2, 1) X(4, 2, 1) X(1, 3, 1) X(2, 3, 1) X(1, 4, 1) X(2, 4, 1) X(4, 4, 1) X(4, 2, 2) X(4, 4, 2)
 
-static const void *group_kernel(int nr, int ipl, int rpl, bool xr)
+static const void *group_kernel(int nr, int ipl, int rpl, bool xr, bool hk = false)
 {
 #define X(NRV, IPLV, RPLV)                                                                     \
     if (nr == NRV && ipl == IPLV && rpl == RPLV)                                               \
         return xr ? reinterpret_cast<const void *>(&k_group<NRV, IPLV, RPLV, true>)            \
+             : hk ? reinterpret_cast<const void *>(&k_group<NRV, IPLV, RPLV, false, true>)     \
                   : reinterpret_cast<const void *>(&k_group<NRV, IPLV, RPLV, false>);
     GROUP_VARIANTS(X)
 #undef X
@@ -2737,9 +2852,18 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
     // the same time.  Workgroups are dealt round-robin over the 8 XCDs, so
     // each XCD must hold its eighth: one XCD (L2-resident hand-offs, xmode)
     // where the blocks fit there, else the whole device
+    // blocks spread over the XCDs: a multiple of 8 of them, so that k_group's
+    // two-level exchange applies (G / 8 blocks per XCD; LPGPU_HIER=0: flat)
+    static int hier_env = -1;
+    if (hier_env < 0) {
+        const char *v = std::getenv("LPGPU_HIER");
+        hier_env = v ? std::atoi(v) : 1;
+    }
     for (int pass = 0; pass < 2; ++pass)
         for (int k = 0; k < nc; ++k) {
-            const long long g = cand[k].g;
+            long long g = cand[k].g;
+            if (pass == 1 && hier_env && !xr && nshard == 1 && g >= 64)
+                g = std::min<long long>((g + 7) / 8 * 8, GROUP_MAXBLOCKS);
             const int rpl = cand[k].rpl;
             const long long cpb = (ld + g - 1) / g, rpb = (rc + g - 1) / g;
             const long long lds = group_lds(rc, ld, g, bmax);
@@ -2753,7 +2877,9 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
                 nr = 4;
                 ipl = ipl <= 2 ? 2 : 4;
             }
-            const void *fn = group_kernel(nr, ipl, rpl, xr != 0);
+            // spread single-device groups: the variant with the two-level exchange
+            const bool hk = pass == 1 && hier_env && !xr && nshard == 1 && g % 8 == 0 && g >= 64;
+            const void *fn = group_kernel(nr, ipl, rpl, xr != 0, hk);
             if (!fn) continue;
             const int per_cu = group_per_cu(fn, (size_t)lds);
             if (per_cu < 1) continue;
@@ -2768,6 +2894,7 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
             G.lds = (size_t)lds;
             G.per_cu = per_cu;
             G.xmode = one ? 1 : 0;
+            G.hk = hk ? 1 : 0;
             return G;
         }
     return GroupGeom{};
@@ -2794,7 +2921,7 @@ hipError_t launch_group(hipStream_t s, const Args &A, const GroupGeom &geo, int 
 {
     if (geo.g == 0 || count < 1 || count > bmax || bmax > BMAX) return hipErrorInvalidValue;
     if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
-    const void *fn = group_kernel(geo.nr, geo.ipl, geo.rpl, xr != 0);
+    const void *fn = group_kernel(geo.nr, geo.ipl, geo.rpl, xr != 0, geo.hk != 0);
     if (!fn) return hipErrorInvalidValue;
     const int xmode = (geo.xmode && !As) ? 1 : 0;
     const dim3 grid((unsigned)(geo.g * (As ? nshard : 1) * (xmode ? 8 : 1)));

@@ -303,7 +303,11 @@ static Args args_of(const lp_handle *h)
     A.spin_max = h->spin_max;
     A.xwait_ms = h->xwait_ms;
     A.fault = 0;
-    A.pad1 = 0;
+    static const int hier = [] {
+        const char *v = std::getenv("LPGPU_HIER");   // A/B: 0 = flat exchange for spread blocks
+        return v ? std::atoi(v) : 1;
+    }();
+    A.hier = hier;
     A.rank = h->rank;
     A.xbuf = h->xbuf;
     A.peer = h->dpeer;
@@ -407,7 +411,7 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMemsetAsync(h->MQ, 0, mqbytes, h->s));
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
-    const size_t gbytes = 3 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);   // k_group summary regions
+    const size_t gbytes = 4 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);   // k_group summary regions
     HCHK(h, hipMalloc(&h->gran, gbytes));
     HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
     HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));

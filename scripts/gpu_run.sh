@@ -343,6 +343,18 @@ for step in "$@"; do
             done
             for f in "$OUT"/t[34]_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 2))"; done ;;
         configs) run configs 600 python bench.py --configs ;;
+        hier)
+            # two-level exchange for spread selection blocks: A/B at cfg4, then phase clocks
+            for rep in 1 2 3; do
+                for H in 0 1; do
+                    LPGPU_HIER=$H run hier_${H}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                done
+            done
+            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
+            LPGPU_LIB=$L run stamps_hier1 300 python scripts/diag_stamps.py tall 32768 8192 64
+            LPGPU_LIB=$L LPGPU_HIER=0 run stamps_hier0 300 python scripts/diag_stamps.py tall 32768 8192 64
+            for f in "$OUT"/hier_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sel', round(d['selection']['us_per_pivot'], 2))"; done
+            grep -H "^avg" "$OUT"/stamps_hier*.log ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

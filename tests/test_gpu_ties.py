@@ -65,3 +65,26 @@ def test_single_device_wide_tie_solve(tie):
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), o.T)
     e.close()
+
+
+@pytest.mark.parametrize("rule", [_lib.RULE_STANDARD, _lib.RULE_MIN_INDEX])
+@pytest.mark.parametrize("tie", [1e-12, 0.3])
+def test_spread_selection_two_level_exchange(rule, tie):
+    """blocks spread over the XCDs (16500 rows: 136 blocks, two own rows per
+    lane) exchange through their XCD's L2 and one summary per XCD
+    (k_group's two-level exchange): with wide bands the group summaries'
+    candidates often lie outside the global band and the kernel rescans a
+    whole XCD group's rows or row-0 columns"""
+    T = gen.tableau("tall", 16500, 40, 36)
+    e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+    e.upload(T)
+    e.set_block(64)
+    e.set_tol(cost_tie=tie, ratio_tie=tie)
+    st, done = e.run(rule, 40)
+    o = F64Tableau(T, {"cost_tie": tie, "ratio_tie": tie})
+    ost, olog = o.run(0 if rule == _lib.RULE_STANDARD else 1, 40)
+    assert done == len(olog)
+    assert e.log().tolist() == olog.tolist()
+    assert np.array_equal(e.download(), o.T)
+    assert e.exchange_path() == (_lib.PATH_PERSISTENT, 0)
+    e.close()
