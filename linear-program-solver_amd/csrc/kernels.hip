@@ -964,7 +964,7 @@ __device__ bool gather_x(const u64 *slots, int n, unsigned tag, unsigned (&w)[NG
 }
 
 // Two-level exchange, level 1 -> 2 (k_group, blocks spread over the XCDs):
-// the first block of XCD group x gathers the group's G8 summaries (logical
+// the last block of XCD group x gathers the group's G8 summaries (logical
 // slots x G8 .. x G8 + G8 - 1, granule-major, L2-resident) and publishes ONE
 // summary of the same format to slot x of the level-2 region (block-major,
 // write-through): l = the group minimum; q, i = the candidate of the group's
@@ -1131,7 +1131,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     // Two-level exchange for blocks spread over the 8 XCDs (single device): the
     // G / 8 blocks of one XCD (b % 8 equal under the round-robin dealing,
     // checked here) exchange their summaries through that XCD's L2 (level 1,
-    // plain stores, granule-major), the XCD's first block combines them into
+    // plain stores, granule-major), the XCD's last block combines them into
     // one summary of the same format and publishes it write-through (level 2),
     // and every block polls the 8 level-2 summaries -- instead of every block
     // polling all G summaries across the XCDs.  Blocks are numbered XCD-major
@@ -1180,7 +1180,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             return true;
         }
         publish(g1, L, tag, wv, n, true, 0);
-        if (b / 8 != 0) return true;
+        if (b / 8 != G8 - 1) return true;      // the group's last block combines (block 0 has its own duties)
         return entering ? hier_combine<NGE>(g1, g2, b % 8, G8, tag, tie, true, &ctl->bar_timeout, A.spin_max)
                         : hier_combine<NGR>(g1, g2, b % 8, G8, tag, tie, false, &ctl->bar_timeout, A.spin_max);
     };
