@@ -212,3 +212,23 @@ def test_phase1_golden_covers_every_outcome():
     assert {fx.get("error") for fx in SMALL["phase1"]} == {None, "IndexError", "ValueError"}
     # phase 1 made drive-out pivots somewhere (artificial basic at value 0)
     assert any(len(fx["init_seq"]) > 0 for fx in SMALL["phase1"] if fx["phase1"]["kind"] == "ge")
+
+
+def test_oracle_under_sanitizers():
+    """oracle/lp_f64.c built with -fsanitize=address,undefined (no recovery)
+    and run over exact-size tableaux (random dyadic LPs, Klee-Minty d=2..8):
+    no sanitizer report, and its solve/scan invariants hold
+    (oracle/sanitize_main.c)."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which(os.environ.get("CC", "gcc")) is None:
+        pytest.skip("no C compiler")
+    root = os.path.join(os.path.dirname(__file__), "..", "oracle")
+    subprocess.run(["make", "-s", "-C", root, "sanitize"], check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    run = subprocess.run([os.path.join(root, "build", "lpf64_sanitize")], capture_output=True,
+                         text=True, timeout=300, env=env)
+    assert run.returncode == 0, run.stdout + run.stderr
+    assert "clean" in run.stdout
