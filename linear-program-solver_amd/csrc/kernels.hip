@@ -2150,7 +2150,7 @@ template <int W, int NB, int SA, int LA = 0>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 8)))
 k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-           int nstrips, long long run)
+           int nstrips, long long run, long long tail)
 {
     constexpr int RW = 4;                        // rows per batch (4 x 4 = 16 values a register)
     constexpr int NM = NB / 4;                   // multiplier registers (4 pivots each)
@@ -2159,25 +2159,23 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
     __shared__ long long sr[NB];
     const int nd = (int)ctl->ndef[grp];          // <= NB (the host's bound)
     if (nd == 0 || ctl->bar_timeout) return;     // nothing deferred / group redone by the host
-    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
-    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
-    const long long r1 = min(rows, r0 + run);
-    if (r0 >= r1) return;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long c0 = (long long)strip * 128;
-    const int lo = min(lane * 2, (int)(ld - c0) - 2);
-    const int lob = lo * 8;
     const int ldb = (int)(ld * 8);
-    const double *Ts = T + c0;
-    double *Tos = Tout + c0;
     if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
-    for (int s = wave; s < NB; s += W)
-        sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
     // this lane's multiplier slot of register c: pivot 4 c + q / 4, row q % 4
     // (q = lane % 16); pivots past nd read pivot nd - 1's (finite; their P is 0)
     const int q = lane & 15, qs = q >> 2, qk = q & 3;
     const int nch = (nd + 3) >> 2;               // chunks holding live pivots
+    // rows [r0, r1) of one strip
+    auto piece = [&](int strip, long long r0, long long r1) {
+    const long long c0 = (long long)strip * 128;
+    const int lo = min(lane * 2, (int)(ld - c0) - 2);
+    const int lob = lo * 8;
+    const double *Ts = T + c0;
+    double *Tos = Tout + c0;
+    for (int s = wave; s < NB; s += W)
+        sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
     // the multipliers of chunk c of the batch at rb (one register)
     auto load_m = [&](long long rb, int c) {
         const int mk = min(qk, (int)(r1 - 1 - rb));
@@ -2256,6 +2254,17 @@ k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const do
         for (int k = 0; k < RW; ++k)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
     }
+    };
+    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
+    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
+    piece(strip, r0, min(rows, r0 + run));
+    if (tail > 0) {                              // as in k_sweep_dp2
+        const long long t0 = (long long)blockIdx.x * tail;
+        if (t0 < rows) {
+            __syncthreads();
+            piece(nstrips, t0, min(rows, t0 + tail));
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2272,7 +2281,7 @@ template <int W, int NB, int SA>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(5, 8)))
 k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
             const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-            int nstrips, long long run)
+            int nstrips, long long run, long long tail)
 {
     constexpr int RW = 4;                        // rows per batch
     constexpr int NM = NB / 4;                   // 4-pivot chunks
@@ -2413,6 +2422,18 @@ k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const d
     const int strip = (int)(blockIdx.x % (unsigned)nstrips);
     const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
     piece(strip, r0, min(rows, r0 + run));
+    // tail > 0: the grid covers strips [0, nstrips) only and the last strip
+    // (the one past them: column n and the row pitch's padding) is dealt out
+    // `tail` rows to every block -- a whole block per run of that thin strip
+    // would leave about one resident slot in nine empty (nstrips + 1 = 65
+    // strips over 512 slots: 7 runs x 65 = 455 blocks)
+    if (tail > 0) {
+        const long long t0 = (long long)blockIdx.x * tail;
+        if (t0 < rows) {                         // block-uniform
+            __syncthreads();                     // every wave is done with sp
+            piece(nstrips, t0, min(rows, t0 + tail));
+        }
+    }
 }
 
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
@@ -2727,20 +2748,37 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
                           : (const void *)&k_sweep_dp2<10, 64, SA>;
         }
         const int bpc = sweep_blocks_per_cu(fn, 64 * wv);
-        long long nrun = (long long)sweep_cus() * bpc / ns;
+        // the last strip (column n and the pitch's padding) spread over all
+        // blocks where the runs are long: the grid then fills every resident
+        // slot (cfg4: 7 x 65 = 455 of 512 -> 8 x 64 = 512, sweep 1055-1072 ->
+        // 985-987 us per 64-pivot launch); at cfg3's 516-row runs the extra
+        // short piece (a P restage + one batch) costs more than the slots
+        // give back (112.1 -> 114.3-114.6 us).  LPGPU_SWEEP_TAIL (A/B):
+        // 1 (default) runs of >= 2048 rows, 2 always, 0 never
+        static int tail_env = -1;
+        if (tail_env < 0) {
+            const char *v = std::getenv("LPGPU_SWEEP_TAIL");
+            tail_env = v ? std::atoi(v) : 1;
+        }
+        const long long slots = (long long)sweep_cus() * bpc;
+        const bool tailed = ns >= 2 && (tail_env == 2 || (tail_env == 1 && A.rows * (ns - 1) >= 2048 * slots));
+        const long long nsg = tailed ? ns - 1 : ns;   // strips with blocks of their own
+        long long nrun = slots / nsg;
         if (nrun < 1) nrun = 1;
         long long run = (A.rows + nrun - 1) / nrun;
         run = (run + RW - 1) / RW * RW;
         nrun = (A.rows + run - 1) / run;
-        const dim3 grid((unsigned)(nrun * ns));
+        const dim3 grid((unsigned)(nrun * nsg));
+        // tail rows per block: a multiple of the batch (the multipliers' 4-row quads)
+        long long tail = tailed ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + RW - 1) / RW * RW : 0;
         const Args *ap = &A;
         const double *T = ap->T, *Pp = ap->P, *Mp = ap->MQ;   // the sweep reads the quad copy
         double *To = ap->T;
         const long long *dRp = ap->dR;
         const Ctl *ctlp = ap->ctl;
         long long ld = ap->ld, rows = ap->rows;
-        int grpv = grp, nsv = (int)ns;
-        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run};
+        int grpv = grp, nsv = (int)nsg;
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail};
         (void)hipExtLaunchKernel(fn, grid, dim3(64 * wv), args, 0, s, e0, e1, 0);
         return hipGetLastError();
     }

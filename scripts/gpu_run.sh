@@ -77,6 +77,15 @@ for step in "$@"; do
                     LPGPU_LIB=$L LPGPU_PIPELINE=0 run bench_${V}_$rep 300 python bench.py --no-cpu-baseline --steps 512 --block ${AB_BLOCK:-16}
                 done
             done ;;
+        tailab)
+            # A/B: k_sweep_dp2's last strip spread over all blocks (LPGPU_SWEEP_TAIL)
+            # and k_sweep_dp2 at 64 pivots (LPGPU_SWEEP_DP=2, cfg4)
+            for rep in 1 2; do
+                for T in 1 0; do
+                    LPGPU_SWEEP_TAIL=$T run bench_tail${T}_$rep 300 python bench.py --no-cpu-baseline
+                    LPGPU_SWEEP_TAIL=$T LPGPU_SWEEP_DP=2 run bench_dp2_tail${T}_$rep 300 python bench.py --no-cpu-baseline --no-cfg3
+                done
+            done ;;
         modes)
             for rep in 1 2; do
                 for B in 16 32; do
