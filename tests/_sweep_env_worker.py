@@ -1,0 +1,41 @@
+"""Child process of test_gpu_r2.py::test_sweep_grid_modes_bit_exact: the
+sweep's grid switches (LPGPU_SWEEP_TAIL, LPGPU_SWEEP_DP) are read once per
+process, so each setting runs here, over several shapes, against the f64
+oracle.  Prints one line per shape and "ALL OK" at the end."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
+sys.path.insert(0, ROOT)
+
+from lpsol_amd import _lib, generators as gen  # noqa: E402
+from oracle.f64 import F64Tableau  # noqa: E402
+
+# (kind, m, ns, pivots, pivots per sweep): strips of 1, 2, 9 and 17 x 128
+# columns, row counts off the 4-row batch, tall and square
+SHAPES = [("tall", 777, 64, 20, 8), ("mixed", 333, 100, 24, 16), ("tall", 4099, 700, 24, 16),
+          ("mixed", 1500, 1000, 30, 48), ("pos", 2050, 2000, 20, 64)]
+
+
+def main():
+    for kind, m, ns, k, block in SHAPES:
+        T = gen.tableau(kind, m, ns, 11)
+        o = F64Tableau(T.copy())
+        _, olog = o.run(0, k)
+        e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+        e.upload(T)
+        e.set_block(block)
+        st, done = e.run(_lib.RULE_STANDARD, k)
+        ok = done == len(olog) and e.log().tolist() == olog.tolist() and np.array_equal(e.download(), o.T)
+        print(kind, m, ns, "pivots", done, "ok" if ok else "MISMATCH", flush=True)
+        e.close()
+        if not ok:
+            sys.exit(1)
+    print("ALL OK")
+
+
+if __name__ == "__main__":
+    main()

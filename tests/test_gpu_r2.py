@@ -205,3 +205,20 @@ def test_json_device_solve_matches_reference(fx, tmp_path):
     u = Tableau(1, 1)
     u.loadFile(str(p))
     assert np.array_equal(u.toArray(), tab.toArray())
+
+
+# ------------------------------------------------- sweep grid switches
+@pytest.mark.parametrize("env", [{"LPGPU_SWEEP_TAIL": "2"}, {"LPGPU_SWEEP_TAIL": "2", "LPGPU_SWEEP_DP": "2"},
+                                 {"LPGPU_SWEEP_TAIL": "0"}], ids=["tail", "tail-dp2", "no-tail"])
+def test_sweep_grid_modes_bit_exact(env):
+    """the sweep's last strip dealt out to every workgroup (on by default only
+    for long runs, cfg4) forced on and off for small shapes, with both sweep
+    kernels: pivots and every row identical to oracle/lp_f64.c (one child
+    process per setting: the switches are read once per process)"""
+    import os
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(__file__), "_sweep_env_worker.py")
+    run = subprocess.run([sys.executable, "-u", worker], env=dict(os.environ, **env), capture_output=True,
+                         text=True, timeout=110)
+    assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
