@@ -77,6 +77,8 @@ for step in "$@"; do
                     LPGPU_LIB=$L LPGPU_PIPELINE=0 run bench_${V}_$rep 300 python bench.py --no-cpu-baseline --steps 512 --block ${AB_BLOCK:-16}
                 done
             done ;;
+        sweepgrid)
+            run sweep_grid 300 python -u -m pytest tests/test_gpu_r2.py -k sweep_grid -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         tailab)
             # A/B: k_sweep_dp2's last strip spread over all blocks (LPGPU_SWEEP_TAIL)
             # and k_sweep_dp2 at 64 pivots (LPGPU_SWEEP_DP=2, cfg4)
