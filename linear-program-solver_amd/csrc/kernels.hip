@@ -997,9 +997,11 @@ __device__ bool hier_combine(const u64 *lvl1, u64 *lvl2, unsigned x, unsigned G8
         o[3] = hi32(q);
         o[4] = entering ? (i & 0x7fffffffu) | (o[4] & 0x80000000u) : i;
     }
-    if (entering) {
-        const long long fn = in ? (long long)(w[0][5] & 0x7fffffffu) : 0x7fffffffLL;
-        o[5] = (unsigned)wave_min_ll(fn) | (o[5] & 0x80000000u);
+    if constexpr (NG > 5) {                      // word 5 exists in entering summaries only
+        if (entering) {
+            const long long fn = in ? (long long)(w[0][5] & 0x7fffffffu) : 0x7fffffffLL;
+            o[5] = (unsigned)wave_min_ll(fn) | (o[5] & 0x80000000u);
+        }
     }
     unsigned wv = 0;
 #pragma unroll
