@@ -2926,7 +2926,12 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, int bmax, int x
             const bool one = pass == 0;
             if (one && !(xcd_on && xr != 1 && nshard == 1 && share == 1 && g <= (long long)per_cu * xcd_cus))
                 continue;
-            if (!one && (g * nshard * share + 7) / 8 > (long long)per_cu * xcd_cus) continue;
+            // ranks sharing a GPU launch their groups unsynchronised, so another
+            // rank's sweep or set-up kernel can hold a slot while this group must
+            // be resident: there, one block slot per CU stays free (4 ranks of
+            // cfg4 on one GPU filled 2 of 2 slots per CU and timed out, round 2)
+            const int per_cu_job = share > 1 ? per_cu - 1 : per_cu;
+            if (!one && (g * nshard * share + 7) / 8 > (long long)per_cu_job * xcd_cus) continue;
             G.g = g;
             G.nr = nr;
             G.ipl = ipl;

@@ -44,6 +44,8 @@ for step in "$@"; do
         dist2)
             # two ranks sharing the one GPU: no RCCL (it refuses that), peer exchange only
             run bench_dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 256 --warmup 32 --no-rccl ;;
+        dist4)
+            run bench_dist4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --steps 256 --warmup 32 --no-rccl ;;
         prof16)
             export TMPDIR=/tmp
             run rocprof16 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof16" -o run -- python3 "$PWD/bench.py" --steps 512 --block 16 --no-cpu-baseline ;;
