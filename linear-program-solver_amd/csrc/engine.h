@@ -86,7 +86,8 @@ struct Ctl {
     unsigned pad;
     unsigned bar[2];     // unused (kept zero)
     unsigned bar_timeout;// set if a k_group exchange gave up (never expected)
-    unsigned pad2;
+    unsigned sel_flags;  // the last persistent selection launch (block 0): 1 every block on one XCD,
+                         // 2 the two-level exchange engaged (k_group), 4 the one-XCD kernel k_sel ran
     // k_group: the loop state at the start of the launch (every block writes
     // the same values before any pivot of the group: a timeout is only seen
     // by a block that ran, so the snapshot is always the failing launch's,
@@ -214,12 +215,19 @@ struct GroupGeom {
     int hk = 0;          // 1: blocks spread over the XCDs, the k_group variant with the two-level exchange
     size_t lds = 0;      // dynamic LDS per block
     int per_cu = 0;      // resident blocks per CU the launch relies on
+    int sel = 0;         // > 0: the one-XCD selection k_sel (select.hip) for up to `sel` pivots per launch
 };
 // rc: local constraint rows (the largest shard's for a sharded job); bmax:
 // pivots per group; xr: 0 single device, 1 row-sharded rank, 2 row-sharded
 // rank that may use one XCD; nshard: in-process shards in one launch; share:
 // processes whose launches must be resident on this device at the same time.
-GroupGeom group_geom(long long rc, long long ld, int bmax, int xr, int nshard, int share);
+GroupGeom group_geom(long long rc, long long ld, long long n, int bmax, int xr, int nshard, int share);
+// the one-XCD selection (select.hip): g <= 64 blocks, one own row per lane,
+// the variable columns 1..n split evenly; g == 0 if the shape does not fit
+GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr);
+hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int grp, int count, int from_erec,
+                      unsigned seq, int xr, int first, int fmode, int frule, long long fcap, hipEvent_t e0,
+                      hipEvent_t e1);
 // one persistent launch selecting up to `count` chained pivots of a group;
 // seq numbers the launches of a handle (1 .. 2^23-1, then wraps to 1): it tags
 // the launch's summaries so no stale granule can match.  xr: one rank of a

@@ -925,11 +925,11 @@ static lpk::GroupGeom persistent_geom_b(lp_handle *h, size_t nmem, int *xr, int 
     *xr = 0;
     lpk::GroupGeom none;
     if (!h->persistent) return none;
-    if (!h->comm) return lpk::group_geom(h->rc, h->ld, bmax, 0, 1, 1);
+    if (!h->comm) return lpk::group_geom(h->rc, h->ld, h->n, bmax, 0, 1, 1);
     if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
     *xr = (nmem == 1 && h->xr_xcd) ? 2 : 1;
-    return lpk::group_geom(rcmax, h->ld, bmax, *xr, (int)nmem, nmem == 1 ? h->share : 1);
+    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 ? h->share : 1);
 }
 
 // Pivots per sweep when the handle says auto (0).  More pivots per sweep cut
@@ -1666,6 +1666,28 @@ extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
     if (!h->stamps) return LP_BAD_ARG;
     HCHK(h, hipMemcpy(out, h->stamps + lpk::BMAX * 16,
                       lpk::GROUP_MAXBLOCKS * lpk::BMAX * 4 * sizeof(long long), hipMemcpyDeviceToHost));
+    return LP_PIVOTED;
+}
+
+// diagnostics: the persistent selection this handle's pivot loops launch and
+// what its last launch found on the device.  out[0..7] = blocks per shard,
+// own columns per lane, own rows per lane, summaries per lane, one-XCD grid,
+// k_group's two-level variant, k_sel's pivot capacity (0: k_group),
+// Ctl::sel_flags of the last launch (1 one XCD, 2 two-level exchange engaged,
+// 4 k_sel); all 0 when the per-pivot kernels run
+extern "C" int lpdiag_geometry(lp_handle *h, long long *out)
+{
+    const Members M = members_of(h);
+    int xr = 0;
+    const lpk::GroupGeom g = persistent_geom(h, M, &xr);
+    out[0] = g.g;
+    out[1] = g.ipl;
+    out[2] = g.rpl;
+    out[3] = g.nr;
+    out[4] = g.xmode;
+    out[5] = g.hk;
+    out[6] = g.sel;
+    out[7] = h->hctl->sel_flags;
     return LP_PIVOTED;
 }
 

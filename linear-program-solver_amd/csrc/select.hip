@@ -1,0 +1,915 @@
+// One-XCD persistent pivot selection (k_sel): every selection of a group of
+// chained pivots in ONE launch whose G <= 64 single-wave workgroups share one
+// XCD -- the cfg3 tableau (4096 x 8192) on one GPU, and each rank's 4096-row
+// shard of cfg4 across eight (BASELINE.json north_star).
+//
+// Same contract as k_group (kernels.hip), rebuilt around what bounds a pivot
+// there -- a chain of dependent latencies (two block exchanges, two dependent
+// memory round trips, two deferred-pivot chains) -- with the per-pivot work
+// on that chain cut down:
+//   * the deferred-pivot chains run from registers: a lane's multipliers of
+//     its own row (M, pivot s of this launch in mreg[s]) stay in VGPRs, and
+//     the other operand of each FMA (P[s][C] for the column, M[R][s] for the
+//     pivot row) is broadcast from lane s % 16 of the lane's 16-lane row by
+//     the FMA itself (v_fmac_f64_dpp row_newbcast) -- no LDS round trip per
+//     pivot on the column side, one 16-byte LDS read per two pivots and
+//     column on the row side (P[s][own column], software-pipelined);
+//   * no select in the chains: a row that was an earlier pivot row s* of the
+//     launch starts from P[s*] and its multipliers of pivots <= s* are zero
+//     (fma(-p, 0, x) == x for finite p), the operations of upd() exactly;
+//   * column 0 (b) is computed by every block: the ratio summary carries the
+//     candidate's pivot element and current b, so every block forms
+//     P[t][0] = b / a itself -- no owner of column 0, the pivot row's
+//     columns 1..n split evenly (cfg3: 64 blocks x 128 columns, two per lane),
+//     and the stall bookkeeping (simplex.py:123-137) runs in every block from
+//     the same values, so the rule and stop flag need no broadcast;
+//   * a block publishes its ratio summary without draining its stores: the
+//     summary carries everything the pivot row needs (the multipliers of
+//     earlier pivots were drained at earlier row-0 publications), and a near
+//     tie that straddles the band is answered by the block that holds it (one
+//     more hand-off) instead of rescans of its stored values;
+//   * the multipliers' sweep copy (MQ) and column 0 are stored once at the
+//     end of the launch, from registers.
+// Every element still gets the float64 operations of oracle/lp_f64.c in the
+// same order (bit-identical tableaux); simplex.py:218-284 (selection),
+// tableau.py:295-308 (pivot), simplex.py:110-148 (solve loop).
+#include "engine.h"
+#include "device.h"
+
+#include <hip/hip_ext.h>
+
+#include <array>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+namespace lpk {
+namespace {
+
+constexpr int SEL_NGR = 7;   // ratio summary: l (2), i, a (2), b (2)
+constexpr int SEL_NGE = 6;   // row-0 summary: l (2), q (2), i, fneg
+constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
+typedef double d16 __attribute__((ext_vector_type(16)));
+
+// ---- deferred-pivot chains --------------------------------------------------
+// x <- fma(-v[lane L of this lane's 16-lane row], m, x): the DPP operand is the
+// broadcast one.  fma(-v, m, x) == fma(-m, v, x) bit for bit (the product is
+// exact before the single rounding), so either operand order is upd()'s.
+// Each block starts with s_nop: the DPP source must not be written by a VALU
+// instruction in the two (five after an EXEC write) cycles before.
+#define SEL_F(L, M) "v_fmac_f64_dpp %0, -%1, %" #M " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
+#define SEL_COL8(L0, L1, L2, L3, L4, L5, L6, L7)                                                      \
+    asm("s_nop 4\n" SEL_F(L0, 2) SEL_F(L1, 3) SEL_F(L2, 4) SEL_F(L3, 5) SEL_F(L4, 6) SEL_F(L5, 7)     \
+            SEL_F(L6, 8) SEL_F(L7, 9)                                                                 \
+        : "+v"(a)                                                                                     \
+        : "v"(v), "v"(mk[o]), "v"(mk[o + 1]), "v"(mk[o + 2]), "v"(mk[o + 3]), "v"(mk[o + 4]),          \
+          "v"(mk[o + 5]), "v"(mk[o + 6]), "v"(mk[o + 7]))
+
+// column chain: a (this lane's row, column C) <- pivots 0..t-1, whole chunks
+// of 8 (pivots t.. of the last chunk: v = 0 and m = 0, exact no-ops)
+template <int NK, int C>
+__device__ __forceinline__ void col_chunk(double &a, double v, const d16 &mk)
+{
+    constexpr int o = 8 * (C & 1);
+    if constexpr (C & 1) SEL_COL8(8, 9, 10, 11, 12, 13, 14, 15);
+    else SEL_COL8(0, 1, 2, 3, 4, 5, 6, 7);
+}
+template <int NK>
+__device__ __forceinline__ void col_chain(double &a, const double (&pk)[NK], const d16 &m0, const d16 &m1,
+                                          const d16 &m2, const d16 &m3, int t)
+{
+    if (t > 0) col_chunk<NK, 0>(a, pk[0], m0);
+    if (t > 8) col_chunk<NK, 1>(a, pk[0], m0);
+    if (t > 16) col_chunk<NK, 2>(a, pk[1], m1);
+    if (t > 24) col_chunk<NK, 3>(a, pk[1], m1);
+    if constexpr (NK > 2) {
+        if (t > 32) col_chunk<NK, 4>(a, pk[2], m2);
+        if (t > 40) col_chunk<NK, 5>(a, pk[2], m2);
+        if (t > 48) col_chunk<NK, 6>(a, pk[3], m3);
+        if (t > 56) col_chunk<NK, 7>(a, pk[3], m3);
+    }
+}
+#undef SEL_COL8
+
+// row chain, pivots 2h, 2h + 1 on the lane's IPL columns: x[k] <- fma(-mr[L], p[k], x[k])
+template <int IPL>
+struct RowPair;
+#define SEL_RF(XI, MI, PI, L) "v_fmac_f64_dpp %" #XI ", -%" #MI ", %" #PI " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
+template <>
+struct RowPair<1> {
+    template <int L0, int L1>
+    static __device__ __forceinline__ void run(double (&x)[1], double mr, const double2 (&p)[1]);
+};
+template <>
+struct RowPair<2> {
+    template <int L0, int L1>
+    static __device__ __forceinline__ void run(double (&x)[2], double mr, const double2 (&p)[2]);
+};
+template <>
+struct RowPair<4> {
+    template <int L0, int L1>
+    static __device__ __forceinline__ void run(double (&x)[4], double mr, const double2 (&p)[4]);
+};
+#define SEL_PAIR_DEF(L0, L1)                                                                              \
+    template <>                                                                                           \
+    __device__ __forceinline__ void RowPair<1>::run<L0, L1>(double (&x)[1], double mr, const double2 (&p)[1]) \
+    {                                                                                                     \
+        asm("s_nop 4\n" SEL_RF(0, 1, 2, L0) SEL_RF(0, 1, 3, L1) : "+v"(x[0]) : "v"(mr), "v"(p[0].x), "v"(p[0].y)); \
+    }                                                                                                     \
+    template <>                                                                                           \
+    __device__ __forceinline__ void RowPair<2>::run<L0, L1>(double (&x)[2], double mr, const double2 (&p)[2]) \
+    {                                                                                                     \
+        asm("s_nop 4\n" SEL_RF(0, 2, 3, L0) SEL_RF(1, 2, 5, L0) SEL_RF(0, 2, 4, L1) SEL_RF(1, 2, 6, L1)    \
+            : "+v"(x[0]), "+v"(x[1])                                                                      \
+            : "v"(mr), "v"(p[0].x), "v"(p[0].y), "v"(p[1].x), "v"(p[1].y));                                \
+    }                                                                                                     \
+    template <>                                                                                           \
+    __device__ __forceinline__ void RowPair<4>::run<L0, L1>(double (&x)[4], double mr, const double2 (&p)[4]) \
+    {                                                                                                     \
+        asm("s_nop 4\n" SEL_RF(0, 4, 5, L0) SEL_RF(1, 4, 7, L0) SEL_RF(2, 4, 9, L0) SEL_RF(3, 4, 11, L0)   \
+                SEL_RF(0, 4, 6, L1) SEL_RF(1, 4, 8, L1) SEL_RF(2, 4, 10, L1) SEL_RF(3, 4, 12, L1)           \
+            : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3])                                              \
+            : "v"(mr), "v"(p[0].x), "v"(p[0].y), "v"(p[1].x), "v"(p[1].y), "v"(p[2].x), "v"(p[2].y),      \
+              "v"(p[3].x), "v"(p[3].y));                                                                  \
+    }
+SEL_PAIR_DEF(0, 1)
+SEL_PAIR_DEF(2, 3)
+SEL_PAIR_DEF(4, 5)
+SEL_PAIR_DEF(6, 7)
+SEL_PAIR_DEF(8, 9)
+SEL_PAIR_DEF(10, 11)
+SEL_PAIR_DEF(12, 13)
+SEL_PAIR_DEF(14, 15)
+#undef SEL_PAIR_DEF
+#undef SEL_RF
+#undef SEL_F
+
+// row chain: x (pivot row, own columns) <- pivots 0..t-1 in pairs; the pivot
+// values P[s][own column] come from LDS (16 bytes = two pivots per read),
+// three pairs ahead of the FMAs in a ring of four (pivots past t: mr = 0 and
+// P = 0; reads past the last pair land in the slack after lP, unused).
+// Unrolled by template recursion: the ring slots and broadcast lanes are
+// compile-time constants.
+template <int IPL, int NB>
+__device__ __forceinline__ void lds_pair(double2 (&r)[IPL], const double *lP, const int (&kc)[IPL], int h)
+{
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) r[k] = *reinterpret_cast<const double2 *>(&lP[kc[k] * (NB + 2) + 2 * h]);
+}
+template <int IPL, int NB, int H>
+__device__ __forceinline__ void row_steps(double (&x)[IPL], const double (&mr)[NB / 16], const double *lP,
+                                          const int (&kc)[IPL], int t, double2 (&ring)[4][IPL])
+{
+    if (2 * H >= t) return;
+    lds_pair<IPL, NB>(ring[(H + 3) & 3], lP, kc, H + 3);
+    // keep the read-ahead: without the barrier the scheduler sinks each read
+    // to its FMAs and every pair waits out a full LDS latency
+    __builtin_amdgcn_sched_barrier(0);
+    RowPair<IPL>::template run<2 * (H & 7), 2 * (H & 7) + 1>(x, mr[H >> 3], ring[H & 3]);
+    if constexpr (H + 1 < NB / 2) row_steps<IPL, NB, H + 1>(x, mr, lP, kc, t, ring);
+}
+template <int IPL, int NB>
+__device__ __forceinline__ void row_chain(double (&x)[IPL], const double (&mr)[NB / 16], const double *lP,
+                                          const int (&kc)[IPL], int t)
+{
+    if (t <= 0) return;
+    double2 ring[4][IPL];
+    lds_pair<IPL, NB>(ring[0], lP, kc, 0);
+    lds_pair<IPL, NB>(ring[1], lP, kc, 1);
+    lds_pair<IPL, NB>(ring[2], lP, kc, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    row_steps<IPL, NB, 0>(x, mr, lP, kc, t, ring);
+}
+
+// Summary regions of k_sel: granule g of block b at [g * 64 + b] (G <= 64):
+// one poll instruction reads granule g of every block (512 contiguous bytes,
+// 4 cache lines), and every granule's address is one register plus an
+// immediate offset (the per-granule addresses of the general layout, kept
+// live across the pivot loop, cost k_sel about 70 VGPRs).
+constexpr int SEL_SLOT = 64;
+// the words of a summary: lane g (< n) stores word g of block b
+__device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, unsigned w, int n, bool fast)
+{
+    if ((int)threadIdx.x < n) st_x(&region[threadIdx.x * SEL_SLOT + b], ((u64)tag << 32) | w, fast);
+}
+// every block's summary (lane l: block min(l, G - 1)); polls until every
+// granule carries `tag`, bounded by spin_max polls (the host then redoes the
+// group on the per-pivot kernels)
+template <int NG>
+__device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[NG], unsigned *timeout_flag,
+                           unsigned spin_max)
+{
+    const u64 *p = base + min((unsigned)threadIdx.x, G - 1);
+    for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const u64 v = ld_sc1(p + g * SEL_SLOT);
+            w[g] = (unsigned)v;
+            ok = ok && (unsigned)(v >> 32) == tag;
+        }
+        if (__all(ok)) return true;
+        if (spins > spin_max) {
+            st_sc1(timeout_flag, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+}  // namespace
+
+// NB: most pivots of a launch (register multipliers); IPL: own columns per
+// lane (cpb <= 64 IPL); XR: one rank of a row-sharded job (leaving row and
+// pivot row exchanged between ranks through the peers' exchange buffers, as
+// in k_group).  first: as k_group's (call start: reset / eager / enter).
+template <int IPL, int NB, bool XR>
+__global__ void __launch_bounds__(GROUP_THREADS)
+k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int first, int fmode, int frule,
+      long long fcap)
+{
+    static_assert(NB % 16 == 0 && NB <= BMAX, "k_sel: pivots per launch");
+    // the grid is 8 x G and only blocks 0, 8, 16, ... work: they share one XCD
+    // under the round-robin dealing of workgroups (speed only: checked below)
+    if (blockIdx.x & 7u) return;
+    constexpr int CS = NB + 2;             // LDS stride of a column's pivot values (16-B reads, no conflicts)
+    constexpr int NK = NB / 16;            // broadcast registers
+    extern __shared__ __attribute__((aligned(16))) double lP[];   // [cpb][CS]: P[s][own column]
+    const unsigned b = blockIdx.x >> 3, G = (unsigned)gper;
+    const int lane = threadIdx.x;
+    const Args &Ar = A;
+    Ctl *ctl = A.ctl;
+    const bool reset = (first & 1) != 0, eager = (first & 2) != 0, enter = (first & 4) != 0;
+    if (b == 0 && lane == 0) *gp(&ctl->ndef[grp]) = 0;
+    if (!reset && (ld_sc1(&ctl->status) != LP_PIVOTED || ld_sc1(&ctl->bar_timeout) != 0u)) return;
+    const long long cap = reset ? fcap : *gp(&ctl->cap);
+    const int mode = reset ? fmode : *gp(&ctl->mode);
+    long long npiv = reset ? 0 : ld_sc1(&ctl->npiv);
+    int rule = reset ? frule : ld_sc1(&ctl->rule);
+    long long nstd = 0, stuck = 0;
+    if (!reset) {
+        nstd = ld_sc1(&ctl->nstd);
+        stuck = ld_sc1(&ctl->stuck);
+    }
+    rule = __builtin_amdgcn_readfirstlane(rule);
+    if (lane == 0) {
+        // the loop state before this group: what a timed-out group is redone from
+        st_sc1(&ctl->g_npiv, npiv);
+        st_sc1(&ctl->g_nstd, nstd);
+        st_sc1(&ctl->g_stuck, stuck);
+        st_sc1(&ctl->g_rule, rule);
+        st_sc1(&ctl->g_seq, seq);
+    }
+    const long long ld = A.ld;
+    // own rows: lane l holds row lr0 + l; own columns: j = jc0 + l + 64 k, a
+    // block's share of the variable columns 1..n (column 0 is every block's)
+    const long long rpb = (A.rc + G - 1) / G;
+    const long long lr0 = 1 + (long long)b * rpb, lr1 = min(lr0 + rpb, A.rows);
+    const long long li = lr0 + lane;
+    const bool own = li < lr1;
+    const long long cpb = (A.n + G - 1) / G;
+    const long long jc0 = 1 + (long long)b * cpb, jc1 = min(jc0 + cpb, A.n + 1);
+    int jk[IPL];
+    bool cok[IPL];
+    int kc[IPL];
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+        jk[k] = (int)jc0 + lane + 64 * k;
+        cok[k] = jk[k] < jc1;
+        kc[k] = (int)min((long long)lane + 64 * k, cpb - 1);
+    }
+    // current row 0 on own columns, row0[0], column 0 of the own row: the
+    // eager copies, or (first launch after an upload) the stored tableau's
+    double l0v[IPL];
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) l0v[k] = cok[k] ? (eager ? *gp(A.T + jk[k]) : *gp(A.row0 + jk[k])) : 0.0;
+    double v0 = eager ? *gp(A.T) : *gp(A.row0);
+    double lcv = own ? (eager ? *gp(A.T + li * ld) : *gp(A.col0 + li)) : 0.0;
+    if (eager) {
+        // the other blocks read row0[C] (a pivot's row-0 multiplier)
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (cok[k]) st_sc1(&A.row0[jk[k]], l0v[k]);
+    }
+    // LDS pivot values start at zero: the chains' padding pivots multiply them by 0
+    for (long long e = lane; e < (cpb * CS + 8) / 2; e += GROUP_THREADS)
+        reinterpret_cast<double2 *>(lP)[e] = make_double2(0.0, 0.0);
+    // summary regions: ratio, row 0, XCD check, rescan answers
+    u64 *grR = A.gran;
+    u64 *grE = A.gran + GROUP_MAXBLOCKS * GSLOT;
+    u64 *grX = A.gran + 2 * GROUP_MAXBLOCKS * GSLOT;
+    u64 *grS = A.gran + 3 * GROUP_MAXBLOCKS * GSLOT;
+    bool fast = false;
+    {
+        // every block publishes its XCD; plain (L2-resident) hand-off stores
+        // only if all match
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        drain_stores();
+        if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | xcc);
+        unsigned wx[1];
+        if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
+            if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
+            return;
+        }
+        const bool same = !((unsigned)lane < G) || wx[0] == xcc;
+        fast = __builtin_amdgcn_readfirstlane(__all(same) ? 1 : 0) != 0;
+    }
+    if (b == 0 && lane == 0) *gp(&ctl->sel_flags) = (fast ? 1u : 0u) | 4u;   // diagnostics
+    double z0 = 0.0;
+    if (reset) {
+        z0 = -v0;                              // obj_val at the start (simplex.py:118)
+        if (b == 0 && lane == 0) {
+            st_x(&ctl->status, (int)LP_PIVOTED, fast);
+            st_x(&ctl->mode, mode, fast);
+            st_x(&ctl->rule, rule, fast);
+            st_x(&ctl->chain, 1, fast);
+            st_x(&ctl->cap, cap, fast);
+            st_x(&ctl->r, -1LL, fast);
+            st_x(&ctl->c, -1LL, fast);
+            st_x(&ctl->npiv, 0LL, fast);
+            st_x(&ctl->nstd, 0LL, fast);
+            st_x(&ctl->stuck, 0LL, fast);
+            st_x(&ctl->z0, z0, fast);
+            st_x(&ctl->ndef[grp ^ 1], 0LL, fast);
+            st_sc1(&ctl->bar_timeout, 0u);
+        }
+    } else {
+        z0 = *gp(&ctl->z0);
+    }
+    // this lane's row: the multiplier of pivot s in m<s / 16>[s % 16]
+    d16 m0 = (d16)0.0, m1 = (d16)0.0, m2 = (d16)0.0, m3 = (d16)0.0;
+    int pstar = -1;                             // the latest pivot of the launch whose row was the lane's
+    long long sRv = -1;                         // lane s: pivot s's local row (-1: another rank's)
+    int status = LP_PIVOTED;
+    int stop = 0;                               // the objective increased (simplex.py:133)
+    int ndone = 0;
+    for (int tv = 0; tv < count; ++tv) {
+        const int t = __builtin_amdgcn_readfirstlane(tv);
+        stamp(Ar, b, t, 0);
+        // ---- entering column
+        long long C;
+        if (t == 0 && !from_erec && !enter) {
+            C = ld_sc1(&ctl->c) + 1;
+        } else {
+            const bool capped = cap >= 0 && npiv >= cap;
+            double el = INFINITY, eq = 0.0;
+            long long ei = NONE, ef = NONE;
+            const bool in = (unsigned)lane < G;
+            if (t == 0 && from_erec) {          // previous launch's summaries (kernel boundary)
+                if (in) {
+                    el = ld_sc1(&A.erec[lane].l);
+                    ei = ld_sc1(&A.erec[lane].i);
+                    eq = ld_sc1(&A.erec[lane].q);
+                    ef = ld_sc1(&A.erec[lane].fneg);
+                }
+            } else {
+                const unsigned etag = t == 0 ? gtag(seq, 0, 0) : gtag(seq, t - 1, 1);
+                if (t == 0) {
+                    // first pivot of a call: every block's summary of its row-0 slice
+                    double vv[IPL], vmin = INFINITY;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        vv[k] = cok[k] ? l0v[k] : INFINITY;
+                        vmin = fmin(vmin, vv[k]);
+                    }
+                    double sel_, seq_;
+                    long long sei_, sfn_;
+                    row0_summary<IPL>(vv, vmin, jc0, A.tol, sel_, sei_, seq_, sfn_);
+                    unsigned wv = 0;
+                    if (lane == 0) wv = lo32(sel_);
+                    else if (lane == 1) wv = hi32(sel_);
+                    else if (lane == 2) wv = lo32(seq_);
+                    else if (lane == 3) wv = hi32(seq_);
+                    else if (lane == 4) wv = idx32(sei_);
+                    else if (lane == 5) wv = idx32(sfn_);
+                    drain_stores();
+                    sel_put(grE, b, etag, wv, SEL_NGE, fast);
+                }
+                unsigned w[SEL_NGE];
+                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                if (in) {
+                    el = mk_d(w[0], w[1]);
+                    eq = mk_d(w[2], w[3]);
+                    ei = un_idx(w[4]);
+                    ef = un_idx(w[5]);
+                }
+            }
+            if (stop || capped) {
+                C = NONE;
+            } else if (rule == LP_RULE_MIN_INDEX) {
+                C = wave_min_ll(ef);
+            } else {
+                const double g = wave_min(el);
+                if (!(g < -A.tol.cost)) {
+                    C = NONE;
+                } else {
+                    const double ethr = tie_band(g, A.tol.cost_tie);
+                    double l1[1] = {el}, q1[1] = {eq};
+                    long long i1[1] = {ei};
+                    C = combine_loaded<1>(l1, i1, q1, G, ethr);
+                    if (C < 0) {                // rare: rescan that block's slice of row 0
+                        const long long k0 = 1 + (-1 - C) * cpb, k1 = min(k0 + cpb, A.n + 1);
+                        long long best = NONE;
+                        for (long long k = k0 + lane; k < k1; k += GROUP_THREADS)
+                            if (ld_sc1(&A.row0[k]) <= ethr) { best = k; break; }
+                        C = wave_min_ll(best);
+                    }
+                }
+            }
+            if (C == NONE) status = stop ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
+        }
+        stamp(Ar, b, t, 1);
+        bstamp(Ar, b, t, 2);
+        if (status != LP_PIVOTED) break;
+        // ---- one round trip: the own rows' elements of column C (a pivot row
+        //      of this launch: P[pstar][C]), P[s][C] of the earlier pivots for
+        //      the broadcasts, row 0's value at C
+        // (every load unconditional and the selects after the last one: a
+        // select right after its load made the compiler wait for each load
+        // in turn -- four round trips instead of one)
+        const double *ap = pstar >= 0 ? A.P + (long long)pstar * ld : A.T + (own ? li : 0) * ld;
+        double a = ld_sc1(ap + C);
+        double pk[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+            pk[k] = ld_sc1(&A.P[(long long)max(min(16 * k + (lane & 15), t - 1), 0) * ld + C]);
+        const double f0 = ld_sc1(&A.row0[C]);
+        a = own ? a : 0.0;
+#pragma unroll
+        for (int k = 0; k < NK; ++k) pk[k] = 16 * k + (lane & 15) < t ? pk[k] : 0.0;
+        if (b == 0 && lane == 0) st_x(&ctl->c, C - 1, fast);
+        stamp(Ar, b, t, 2);
+        if (STAMPS && A.stamps) {   // diagnostic: the column elements have arrived
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            bstamp(Ar, b, t, 3);
+            stamp(Ar, b, t, 3);
+        }
+        col_chain<NK>(a, pk, m0, m1, m2, m3, t);
+        // M[t] of the own rows: read by later pivots' row chains (drained with
+        // this pivot's row-0 publication, not with the ratio summary)
+        if (own) st_x(&A.M[mi(A.rows, li, t)], a, fast);
+        if (b == 0 && lane == 0) {            // row 0's multiplier (+ the sweep's copy)
+            st_x(&A.M[mi(A.rows, 0, t)], f0, fast);
+            *gp(&A.MQ[mq(0, t)]) = f0;
+        }
+        // ---- ratio test over the own rows
+        bool okq;
+        const double q = row_ratio(a, lcv, A.tol, okq);
+        okq = okq && own;
+        const double lb = wave_min(okq ? q : INFINITY);
+        long long ib = NONE;
+        double ab = 0.0, bb = 0.0;
+        if (lb < INFINITY) {
+            const u64 mask = __ballot(okq && q <= tie_band(lb, A.tol.ratio_tie));
+            const int f = __builtin_ctzll(mask);
+            ib = lr0 + f;
+            ab = rl_d(lo32(a), hi32(a), f);
+            bb = rl_d(lo32(lcv), hi32(lcv), f);
+        }
+        stamp(Ar, b, t, 4);
+        if (!(A.fault == t + 1 && b == min(1u, G - 1))) {   // fault injection (tests): block 1 (0) never publishes
+            unsigned wv = idx32(ib);
+            if (lane == 0) wv = lo32(lb);
+            else if (lane == 1) wv = hi32(lb);
+            else if (lane == 3) wv = lo32(ab);
+            else if (lane == 4) wv = hi32(ab);
+            else if (lane == 5) wv = lo32(bb);
+            else if (lane == 6) wv = hi32(bb);
+            sel_put(grR, b, gtag(seq, t, 0), wv, SEL_NGR, fast);
+        }
+        bstamp(Ar, b, t, 0);
+        stamp(Ar, b, t, 5);
+        // the multiplier into its register while the summaries travel
+        {
+            const int u = t & 15;
+            switch (t >> 4) {
+            case 0: m0[u] = a; break;
+            case 1: m1[u] = a; break;
+            case 2: if constexpr (NK > 2) m2[u] = a; break;
+            default: if constexpr (NK > 3) m3[u] = a; break;
+            }
+        }
+
+        // ---- leaving row (combine the ratio summaries)
+        unsigned w[SEL_NGR];
+        if (!sel_gather<SEL_NGR>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max)) {
+            status = LP_DEVICE_ERROR;
+            break;
+        }
+        stamp(Ar, b, t, 6);
+        const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
+        const double g = wave_min(rl);
+        long long R = NONE;                   // this device's leaving row (XR: its candidate)
+        double aR = 0.0, bR = 0.0;
+        if (g < INFINITY) {
+            const double thr = tie_band(g, A.tol.ratio_tie);
+            const int bs = __builtin_ctzll(__ballot((unsigned)lane < G && rl <= thr));
+            aR = rl_d(w[3], w[4], bs);
+            bR = rl_d(w[5], w[6], bs);
+            bool okr;
+            const double qr = row_ratio(aR, bR, A.tol, okr);
+            if (okr && qr <= thr) {
+                R = un_idx(rl32(w[2], bs));
+            } else {
+                // rare: block bs's first row inside the global band is not its
+                // candidate; it answers with that row (one more hand-off)
+                const unsigned stag = gtag(seq, t, 4);
+                if (b == (unsigned)bs) {
+                    const int f = __builtin_ctzll(__ballot(okq && q <= thr));
+                    const double af = rl_d(lo32(a), hi32(a), f), bf = rl_d(lo32(lcv), hi32(lcv), f);
+                    unsigned wv = 0;
+                    if (lane == 0) wv = (unsigned)(lr0 + f);
+                    else if (lane == 1) wv = lo32(af);
+                    else if (lane == 2) wv = hi32(af);
+                    else if (lane == 3) wv = lo32(bf);
+                    else if (lane == 4) wv = hi32(bf);
+                    sel_put(grS, 0, stag, wv, SEL_NGS, fast);
+                }
+                unsigned y[SEL_NGS];
+                if (!sel_gather<SEL_NGS>(grS, 1, stag, y, &ctl->bar_timeout, A.spin_max)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                R = (long long)rl32(y[0], 0);
+                aR = rl_d(y[1], y[2], 0);
+                bR = rl_d(y[3], y[4], 0);
+            }
+        } else if (!XR) {
+            status = LP_UNBOUNDED;
+            break;
+        }
+        stamp(Ar, b, t, 7);
+        // ---- pivot row on the own columns: prow(Rl, av) = current values of
+        //      local row Rl (stored row, or P[s*] if it was pivot row s* of
+        //      this launch, + the later pivots of the launch) / av
+        double pv[IPL];
+        auto prow = [&](long long Rl, double avv) {
+            const u64 rp = __ballot(lane < t && sRv == Rl);
+            const int sst = rp ? 63 - __builtin_clzll(rp) : -1;   // uniform
+            // every load issued before any select (see the column's)
+            double x[IPL];
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) x[k] = *gp(A.T + Rl * ld + min(jk[k], (int)A.n));
+            double mr[NK];
+#pragma unroll
+            for (int k = 0; k < NK; ++k)
+                mr[k] = ld_sc1(&A.M[mi(A.rows, Rl, max(min(16 * k + (lane & 15), t - 1), 0))]);
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) x[k] = sst >= 0 ? lP[kc[k] * CS + sst] : (cok[k] ? x[k] : 0.0);
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int s = 16 * k + (lane & 15);
+                mr[k] = (s < t && s > sst) ? mr[k] : 0.0;
+            }
+            if (STAMPS && A.stamps) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                stamp(Ar, b, t, 8);
+            }
+            row_chain<IPL, NB>(x, mr, lP, kc, t);
+            if (STAMPS && A.stamps) {
+                asm volatile("" ::"v"(x[0]), "v"(x[IPL - 1]));
+                stamp(Ar, b, t, 12);
+            }
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) pv[k] = (jk[k] == C) ? 1.0 : x[k] / avv;
+            if (STAMPS && A.stamps) {
+                asm volatile("" ::"v"(pv[0]), "v"(pv[IPL - 1]));
+                stamp(Ar, b, t, 13);
+            }
+        };
+        bool win = true;                      // this rank holds the leaving row
+        long long rglob = R == NONE ? -1 : R - 1 + A.rb;
+        if constexpr (XR) {
+            // ---- leaving row across ranks (as k_group): every rank sends
+            //      (local minimum, global row, pivot element, b) to all ranks
+            //      and, without waiting for the verdict, its candidate's
+            //      normalised row on every block's columns
+            const int par = t & 1;
+            const int N = A.nranks;
+            const unsigned long long xticks = (unsigned long long)A.xwait_ms * 100000ull;
+            u64 *xsl = A.xbuf + par * XS_SUM_PAR;
+            if (b == 0 && lane < SEL_NGR) {
+                const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
+                unsigned wv = 0;
+                if (lane == 0) wv = lo32(g);
+                else if (lane == 1) wv = hi32(g);
+                else if (lane == 2) wv = R == NONE ? 0xffffffffu : (unsigned)rglob;
+                else if (lane == 3) wv = lo32(aR);
+                else if (lane == 4) wv = hi32(aR);
+                else if (lane == 5) wv = lo32(bR);
+                else wv = hi32(bR);
+                for (int p = 0; p < N; ++p)
+                    st_sys(&(*gp(A.peer + p))[par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
+            }
+            auto send_row = [&](int ph) {
+                const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
+                for (int p = 0; p < N; ++p) {
+                    if (p == A.rank) continue;
+                    u64 *dst = (*gp(A.peer + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
+                               (long long)b * XS_PROW_BLOCK;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        const int kk = lane + 64 * k;
+                        if (cok[k]) {
+                            st_sys(&dst[2 * kk], tg | lo32(pv[k]));
+                            st_sys(&dst[2 * kk + 1], tg | hi32(pv[k]));
+                        }
+                    }
+                }
+            };
+            if (R != NONE) {
+                prow(R, aR);
+                send_row(3);
+            }
+            unsigned x[SEL_NGR];
+            if (!gather_x<SEL_NGR>(xsl, N, gtag(seq, t, 2), x, &ctl->bar_timeout, xticks)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
+            const double lp = lane < N ? mk_d(x[0], x[1]) : INFINITY;
+            const double gg = wave_min(lp);
+            if (!(gg < INFINITY)) {
+                status = LP_UNBOUNDED;
+                break;
+            }
+            const double thr = tie_band(gg, A.tol.ratio_tie);
+            const int ps = __builtin_ctzll(__ballot(lane < N && lp <= thr));
+            double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
+            bool okp;
+            const double qs = row_ratio(as, bs, A.tol, okp);
+            long long rg;
+            int ph = 3;                       // the tag of the winner's row slices
+            if (okp && qs <= thr) {
+                rg = (long long)rl32(x[2], ps);
+            } else {
+                // rare: a near-tie straddles the band across ranks.  Rank ps
+                // finds its first row inside it (each block offers its first
+                // own row, block 0 sends the lowest to every rank) and ships
+                // that row's normalised values instead of its candidate's
+                if (A.rank == ps) {
+                    const u64 mk = __ballot(okq && q <= thr);
+                    const int fr = mk ? __builtin_ctzll(mk) : 0;
+                    const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
+                    u64 *loc = A.xbuf + XS_PROW + 2LL * N * XS_PROW_RANK;
+                    if (lane < SEL_NGS) {
+                        const unsigned wv = lane == 0 ? (mk ? (unsigned)(lr0 + fr) : 0x7fffffffu)
+                                          : lane == 1 ? lo32(ar) : lane == 2 ? hi32(ar)
+                                          : lane == 3 ? lo32(br) : hi32(br);
+                        st_sc1(&loc[b * 8 + lane], ((u64)gtag(seq, t, 4) << 32) | wv);
+                    }
+                    unsigned wl[1][SEL_NGS];
+                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout, A.spin_max)) {
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wl[0][0] != 0x7fffffffu));
+                    const unsigned r0w = rl32(wl[0][0], bf), a0 = rl32(wl[0][1], bf), a1 = rl32(wl[0][2], bf),
+                                   b0 = rl32(wl[0][3], bf), b1 = rl32(wl[0][4], bf);
+                    if (b == 0 && lane < SEL_NGS) {
+                        const unsigned wv = lane == 0 ? (unsigned)((long long)r0w - 1 + A.rb)
+                                          : lane == 1 ? a0 : lane == 2 ? a1 : lane == 3 ? b0 : b1;
+                        for (int p = 0; p < N; ++p)
+                            st_sys(&(*gp(A.peer + p))[par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
+                                   ((u64)gtag(seq, t, 5) << 32) | wv);
+                    }
+                }
+                unsigned y[SEL_NGS];
+                if (!gather_x<SEL_NGS>(xsl + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctl->bar_timeout, xticks)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                rg = (long long)__builtin_amdgcn_readfirstlane(y[0]);
+                as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
+                bs = mk_d(__builtin_amdgcn_readfirstlane(y[3]), __builtin_amdgcn_readfirstlane(y[4]));
+                ph = 6;
+                if (A.rank == ps) {
+                    prow(rg - A.rb + 1, as);
+                    send_row(6);
+                }
+            }
+            win = A.rank == ps;
+            rglob = rg;
+            R = win ? rg - A.rb + 1 : -1;
+            aR = as;
+            bR = bs;
+            if (!win) {
+                // the winning rank's block b sent these columns
+                const u64 *src = A.xbuf + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
+                                 (long long)b * XS_PROW_BLOCK;
+                const unsigned tg = gtag(seq, t, ph);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    bool ok = true;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        const int kk = kc[k];
+                        const u64 lo = ld_sys(&src[2 * kk]), hi = ld_sys(&src[2 * kk + 1]);
+                        pv[k] = mk_d((unsigned)lo, (unsigned)hi);
+                        ok = ok && (!cok[k] || ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
+                    }
+                    if (__all(ok)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
+                        st_sc1(&ctl->bar_timeout, 1u);
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (status != LP_PIVOTED) break;
+            }
+        } else {
+            prow(R, aR);
+        }
+        // ---- P[t], row 0 and column 0 (every block: p0 = b / a)
+        const double p0 = bR / aR;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (cok[k]) st_x(&A.P[t * ld + jk[k]], pv[k], fast);
+        double vn[IPL], vv[IPL], vmin = INFINITY;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            vn[k] = upd(0, -1, f0, pv[k], l0v[k]);
+            vv[k] = cok[k] ? vn[k] : INFINITY;
+            vmin = fmin(vmin, vv[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (cok[k]) st_x(&A.row0[jk[k]], vn[k], fast);
+        if (b == 0 && lane == 0) *gp(&A.P[t * ld]) = p0;   // read after the launch (sweep)
+#pragma unroll
+        for (int k = 0; k < IPL; ++k) {
+            if (cok[k]) lP[kc[k] * CS + t] = pv[k];
+            l0v[k] = vn[k];
+        }
+        v0 = upd(0, -1, f0, p0, v0);
+        stamp(Ar, b, t, 9);
+        double el, eq;
+        long long ei, efn;
+        row0_summary<IPL>(vv, vmin, jc0, A.tol, el, ei, eq, efn);
+        // stall bookkeeping (simplex.py:132-137), min-index switch (:123,138)
+        // and the objective check (:133): every block, from the same values
+        if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
+            nstd += 1;
+            const double z = -v0;
+            const double band = A.tol.stall * fmax(1.0, fabs(z0));
+            if (z - z0 > band) stop = 1;
+            if (fabs(z - z0) <= band) stuck += 1;
+            else stuck = 0;
+            if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
+        }
+        stamp(Ar, b, t, 10);
+        {
+            unsigned wv = 0;
+            if (lane == 0) wv = lo32(el);
+            else if (lane == 1) wv = hi32(el);
+            else if (lane == 2) wv = lo32(eq);
+            else if (lane == 3) wv = hi32(eq);
+            else if (lane == 4) wv = idx32(ei);
+            else if (lane == 5) wv = idx32(efn);
+            drain_stores();
+            sel_put(grE, b, gtag(seq, t, 1), wv, SEL_NGE, fast);
+        }
+        bstamp(Ar, b, t, 1);
+        stamp(Ar, b, t, 11);
+        // ---- while the summaries travel: column 0 of the own rows (this
+        //      pivot's multiplier is a), the pivot row's register state, records
+        if (own) lcv = (li == R) ? p0 : fma(-a, p0, lcv);
+        if (R >= lr0 && R < lr1) {            // uniform: the leaving row is one of this block's
+            const bool mine = li == R;
+            m0 = mine ? (d16)0.0 : m0;
+            if (t >= 16) m1 = mine ? (d16)0.0 : m1;
+            if (NK > 2 && t >= 32) m2 = mine ? (d16)0.0 : m2;
+            if (NK > 3 && t >= 48) m3 = mine ? (d16)0.0 : m3;
+            if (mine) pstar = t;
+        }
+        if (lane == t) sRv = R;
+        if (b == G - 1 && lane < 7) {
+            long long *adr = &A.dR[t];
+            long long val = R;
+            if (lane == 1) { adr = &A.dC[t]; val = C; }
+            else if (lane == 2) { adr = &ctl->r; val = rglob; }
+            else if (lane == 3) { adr = &ctl->npiv; val = npiv + 1; }
+            else if (lane == 4) { adr = &ctl->ndef[grp]; val = t + 1; }
+            else if (lane == 5) { adr = A.log + 2 * min(npiv, A.logcap - 1); val = rglob; }
+            else if (lane == 6) { adr = A.log + 2 * min(npiv, A.logcap - 1) + 1; val = C - 1; }
+            if (lane < 5 || npiv < A.logcap) st_x(adr, val, fast);
+        }
+        if (b == 0 && lane == 0 && mode == MODE_SOLVE) {
+            st_x(&ctl->nstd, nstd, fast);
+            st_x(&ctl->stuck, stuck, fast);
+            st_x(&ctl->rule, rule, fast);
+        }
+        if (t == count - 1 && lane == 0) {    // the next launch reads plain summaries
+            st_x(&A.erec[b].l, el, fast);
+            st_x(&A.erec[b].i, ei, fast);
+            st_x(&A.erec[b].q, eq, fast);
+            st_x(&A.erec[b].fneg, efn, fast);
+        }
+        ++npiv;
+        ++ndone;
+    }
+    // the sweep's copy of the launch's multipliers (MQ, 4-row quads), column 0
+    // of the own rows and row 0 / column 0's corner: read after the launch
+    {
+        const int nds = __builtin_amdgcn_readfirstlane(ndone);
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            if (s < nds && own) {
+                const d16 &mk = (s >> 4) == 0 ? m0 : (s >> 4) == 1 ? m1 : (s >> 4) == 2 ? m2 : m3;
+                *gp(&A.MQ[mq(li, s)]) = mk[s & 15];
+            }
+        if (own) *gp(&A.col0[li]) = lcv;
+        if (b == 0 && lane == 0) {
+            *gp(&A.row0[0]) = v0;
+            *gp(&A.col0[0]) = v0;
+        }
+    }
+    if (b == 0 && lane == 0) {
+        // an increase at the launch's last pivot: nothing read the flag yet
+        if (stop && status == LP_PIVOTED) status = LP_OBJ_INCREASED;
+        if (status != LP_PIVOTED) st_sc1(&ctl->status, status);
+    }
+}
+
+// ---- geometry and launch ----------------------------------------------------
+namespace {
+
+const void *sel_kernel(int ipl, int nb, bool xr)
+{
+#define SEL_K(I, N) (xr ? reinterpret_cast<const void *>(&k_sel<I, N, true>) \
+                        : reinterpret_cast<const void *>(&k_sel<I, N, false>))
+    if (nb == 32) return ipl == 1 ? SEL_K(1, 32) : ipl == 2 ? SEL_K(2, 32) : SEL_K(4, 32);
+    return ipl == 1 ? SEL_K(1, 64) : ipl == 2 ? SEL_K(2, 64) : SEL_K(4, 64);
+#undef SEL_K
+}
+
+int sel_per_cu(const void *fn, size_t lds)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, GROUP_THREADS, lds) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    // every block's LDS rounded up to 2 KB (allocation granule and slack),
+    // one block less than the runtime's answer unless LDS is the limit
+    // (kernels.hip group_per_cu)
+    const long long per = ((long long)lds + 2047) / 2048 * 2048;
+    const long long lds_cap = (long long)(160 * 1024) / per;
+    if (n >= lds_cap) return (int)lds_cap;
+    return n - 1;
+}
+
+}  // namespace
+
+GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr)
+{
+    GroupGeom G;
+    static int on = -1;
+    if (on < 0) {
+        const char *v = std::getenv("LPGPU_SEL");   // A/B: 0 = k_group only
+        on = v ? std::atoi(v) : 1;
+    }
+    if (!on || rc < 1 || n < 1 || bmax < 1 || bmax > BMAX) return G;
+    const long long grows = (rc + 63) / 64;
+    long long g = std::max(grows, (n + 255) / 256);
+    if (g > 64) return G;
+    const long long cpb = (n + g - 1) / g;
+    int ipl = (int)((cpb + 63) / 64);
+    if (ipl == 3) ipl = 4;
+    if (ipl > 4) return G;
+    const int nb = bmax <= 32 ? 32 : 64;
+    const size_t lds = ((size_t)cpb * (nb + 2) + 8) * sizeof(double);   // + the row chain's read-ahead slack
+    const void *fn = sel_kernel(ipl, nb, xr);
+    const int per_cu = sel_per_cu(fn, lds);
+    if (per_cu < 1 || g > (long long)per_cu * xcd_cus) return G;
+    G.g = g;
+    G.nr = 1;
+    G.ipl = ipl;
+    G.rpl = 1;
+    G.xmode = 1;
+    G.sel = nb;
+    G.lds = lds;
+    G.per_cu = per_cu;
+    return G;
+}
+
+hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int grp, int count, int from_erec,
+                      unsigned seq, int xr, int first, int fmode, int frule, long long fcap, hipEvent_t e0,
+                      hipEvent_t e1)
+{
+    if (geo.g == 0 || geo.sel == 0 || count < 1 || count > geo.sel) return hipErrorInvalidValue;
+    if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
+    if (A.rc > 64 * geo.g || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
+    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0);
+    const dim3 grid((unsigned)(geo.g * 8));
+    Args a0 = A;
+    int gper = (int)geo.g;
+    void *args[] = {&a0, &gper, &grp, &count, &from_erec, &seq, &first, &fmode, &frule, &fcap};
+    return hipExtLaunchKernel(fn, grid, dim3(GROUP_THREADS), args, geo.lds, s, e0, e1, 0);
+}
+
+}  // namespace lpk

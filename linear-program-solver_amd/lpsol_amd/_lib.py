@@ -311,6 +311,18 @@ class Engine:
         """pivots deferred into one sweep of the tableau (1..64; 0 = auto)"""
         self._check(self.lib.lp_set_block(self.h, int(pivots_per_sweep)), self.h)
 
+    def geometry(self) -> dict:
+        """diagnostics (lpdiag_geometry): the persistent selection's launch
+        geometry for this handle and what its last launch found on the device"""
+        out = (C.c_longlong * 8)()
+        self._check(self.lib.lpdiag_geometry(self.h, out), self.h)
+        keys = ("blocks", "ipl", "rpl", "nr", "one_xcd_grid", "two_level_variant", "sel", "flags")
+        d = dict(zip(keys, list(out)))
+        d["kernel"] = "none" if d["blocks"] == 0 else "k_sel" if d["sel"] else "k_group"
+        d["on_one_xcd"] = bool(d["flags"] & 1)
+        d["two_level_engaged"] = bool(d["flags"] & 2)
+        return d
+
     def get_block(self) -> int:
         """pivots per sweep in use (the auto choice resolved)"""
         b = C.c_int()

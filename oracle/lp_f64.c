@@ -63,6 +63,9 @@ int lpf_pivot(double *T, int64_t m, int64_t n, int64_t ld, int64_t r, int64_t c)
     if (a == 0.0) return LP_ZERO_PIVOT;
     for (int64_t j = 0; j <= n; ++j) p[j] = p[j] / a;
     p[C] = 1.0;
+    /* rows are independent: split over host threads for the headline sizes
+       (each element gets the same operations whichever thread runs it) */
+#pragma omp parallel for schedule(static) if ((m + 1) * (n + 1) > (1 << 22))
     for (int64_t i = 0; i <= m; ++i) {
         if (i == R) continue;
         double *t = row(T, ld, i);

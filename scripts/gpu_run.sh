@@ -368,6 +368,23 @@ for step in "$@"; do
             LPGPU_LIB=$L LPGPU_HIER=0 run stamps_hier0 300 python scripts/diag_stamps.py tall 32768 8192 64
             for f in "$OUT"/hier_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sel', round(d['selection']['us_per_pivot'], 2))"; done
             grep -H "^avg" "$OUT"/stamps_hier*.log ;;
+        r3t)
+            # round 3: cfg3 at 48 / 64 pivots per sweep, cfg4 default, stamps of cfg3 (k_sel)
+            for rep in 1 2; do
+                for B in 48 64; do
+                    run t3b${B}_$rep 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4 --block $B
+                done
+                run t4_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+            done
+            for f in "$OUT"/t3b*_*.log "$OUT"/t4_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 2))"; done
+            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
+            LPGPU_LIB=$L run stamps3_48 300 python scripts/diag_stamps.py mixed 4096 4096 48
+            LPGPU_LIB=$L run stamps3_64 300 python scripts/diag_stamps.py mixed 4096 4096 64
+            grep -H "^avg\|^pcomp" "$OUT"/stamps3_*.log ;;
+        r3f)
+            run r3f 300 python -u -m pytest tests/test_gpu_r2.py -k timeout -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        r3p)
+            run r3p 600 python -u -m pytest tests/test_gpu_r3.py -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -5,6 +5,7 @@ Run from the repo root (needs /root/reference, read-only):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--big]
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --extra   # r2.json only
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline 10   # r3.json only
 
 It imports the reference, drives its own ``Tableau``/``Simplex`` on inputs
 from this repo's generator (``lpsol_amd.generators``) or on hand-built LPs,
@@ -327,14 +328,31 @@ def extra_main():
         json.dump(out, f, separators=(",", ":"))
 
 
+def headline_main(k: int):
+    """tests/golden/r3.json: a prefix of the reference's own standard-rule
+    pivot sequence on the benchmark's cfg3 tableau (4096 x 8192, G_mixed seed
+    3; bench.py WORKLOADS), with the exact objective after it.  About 90 s per
+    pivot of the reference on one core; the oracle check is skipped (it would
+    double that) -- the GPU test compares the engine with this directly."""
+    spec = {"gen": {"kind": "mixed", "m": 4096, "ns": 4096, "seed": 3}}
+    fx = standard_k_fixture(f"cfg3_mixed_4096x4096_s3_k{k}", spec, k, check_oracle=False)
+    with open(os.path.join(OUT, "r3.json"), "w") as f:
+        json.dump({"standard_k": [fx]}, f, separators=(",", ":"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
     ap.add_argument("--extra", action="store_true",
                     help="only tests/golden/r2.json (solve assertions, saveJson round trips)")
+    ap.add_argument("--headline", type=int, default=0, metavar="K",
+                    help="only tests/golden/r3.json: K reference pivots on the cfg3 bench tableau")
     args = ap.parse_args()
     if args.extra:
         extra_main()
+        return
+    if args.headline:
+        headline_main(args.headline)
         return
 
     small = {"kat": [kat_fixture()], "solve": [], "standard_k": [], "selection": [], "phase1": []}
