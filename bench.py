@@ -80,7 +80,7 @@ def workload(name: str, nranks: int, rank: int):
 
 
 SRC_FILES = [os.path.join(ROOT, "linear-program-solver_amd", "csrc", f)
-             for f in ("kernels.hip", "lpgpu.cpp", "engine.h", "Makefile")] + [
+             for f in ("kernels.hip", "select.hip", "lpgpu.cpp", "engine.h", "device.h", "Makefile")] + [
     os.path.join(ROOT, "include", "lpgpu.h")]
 
 
@@ -122,17 +122,56 @@ def load_traffic(path: str | None, block: int, workload_name: str, digest: str):
     return None
 
 
-def cpu_baseline(name: str, seconds_target: float = 15.0) -> dict:
+def first_pivots(name: str, k: int, device: int) -> list[tuple[int, int]]:
+    """the workload's first k standard-rule pivots (global row, column), from
+    the engine (bit-identical to the f64 oracle's, tests/test_gpu_r3.py)"""
+    kind, m, ns, n, _, _ = workload(name, 1, 0)
+    e = _lib.Engine(m, n, device=device)
+    upload([e], kind, m, ns, [(0, m)])
+    e.run(_lib.RULE_STANDARD, k)
+    seq = [(int(r), int(c)) for r, c in e.log()]
+    e.close()
+    return seq
+
+
+def _time_dense_pivot(sub, r_local: int, c: int, rows_of, nrows: int, seconds_target: float):
+    """seconds per row of oracle/exact.py's dense pivot (the reference's row
+    operations over every column, tableau.py:254-308) on growing slices of
+    the sample rows (rows_of(i0, i1) -> exact rows); returns (seconds per
+    row, rows timed, seconds)"""
+    from oracle import exact
+    total, done, S, i0 = 0.0, 0, 8, 0
+    t0 = time.perf_counter()
+    while total < seconds_target and i0 < nrows:
+        blk = rows_of(i0, min(i0 + S, nrows))
+        T = [list(sub[0]), list(sub[r_local])] + [list(r) for r in blk]
+        t1 = time.perf_counter()
+        exact.pivot_dense(T, 0, c)
+        total += time.perf_counter() - t1
+        done += len(blk)
+        i0 += S
+        S = min(2 * S, 256)
+        if time.perf_counter() - t0 > 3 * seconds_target:
+            break
+    return total / max(done, 1), done, total
+
+
+def cpu_baseline(name: str, seconds_target: float = 15.0, seq=None, k_mid: int = 16) -> dict:
     """The reference's algorithm on one host core: oracle/exact.py's
     Fraction restatement of Tableau.pivot in the reference's own order of
     operations (rowDiv, rowAddToObj, then rowSub over EVERY column of every
-    other row, tableau.py:254-308), on the first standard-rule pivot of the
-    workload, applied to a bounded sample of rows and scaled to all rows."""
+    other row, tableau.py:254-308), timed on a bounded sample of rows and
+    scaled to all rows, at two points of the run: pivot #1 (dyadic inputs,
+    the smallest denominators) and pivot #(k_mid + 1), whose exact state is
+    obtained by replaying the first k_mid pivots (``seq``, the engine's) on
+    row 0, the pivot rows and the sample rows -- the Fractions' denominators
+    grow with every pivot, and so does the reference's cost."""
     from oracle import exact
     kind, m, ns, _ = WORKLOADS[name]
+    budget = seconds_target / (2 if seq else 1)
+    # pivot #1: its entering column and leaving row from the whole column (numpy)
     T0 = gen.rows(kind, m, ns, SEED, 0, 1)
     c = int(np.argmin(T0[0, 1:]))
-    # the leaving row from the whole column (cheap; numpy)
     col = np.empty(m)
     b = np.empty(m)
     for a in range(0, m, 4096):
@@ -142,30 +181,46 @@ def cpu_baseline(name: str, seconds_target: float = 15.0) -> dict:
     with np.errstate(divide="ignore", invalid="ignore"):
         q = np.where(col > 0, b / np.where(col > 0, col, 1), np.inf)
     r = int(np.argmin(q))
-    prow = gen.rows(kind, m, ns, SEED, 1 + r, 2 + r)
-    total, rows_done, S, i0 = 0.0, 0, 16, 0
-    t0 = time.perf_counter()
-    while total < seconds_target and i0 + S <= m:
-        pick = [i for i in range(i0, i0 + S) if i != r]
-        blk = gen.rows(kind, m, ns, SEED, 1 + i0, 1 + i0 + S)
-        sub = exact.from_array(np.vstack([T0, prow, blk[[i - i0 for i in pick]]]))
-        t1 = time.perf_counter()
-        exact.pivot_dense(sub, 0, c)
-        total += time.perf_counter() - t1
-        rows_done += len(pick)
-        i0 += S
-        S = min(2 * S, 256)
-        if time.perf_counter() - t0 > 3 * seconds_target:
-            break
-    # the sample's other rows (+ row 0 and the pivot row per chunk, left out:
-    # conservative) -> seconds for the m + 1 rows of a whole pivot
-    sec = total / rows_done * (m + 1)
-    return {"value": 1.0 / sec, "unit": "pivots/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle/exact.py pivot_dense (the reference's Fraction row operations, "
-                       f"every column) on pivot #1 of {name}, {rows_done} of {m + 1} rows "
-                       f"({total:.1f} s on one core), scaled to all rows; host has "
-                       f"{os.cpu_count()} cores"),
-            "seconds_per_pivot": sec}
+    picks = [i for i in range(0, min(m, 4096)) if i != r]
+    sub = exact.from_array(np.vstack([T0, gen.rows(kind, m, ns, SEED, 1 + r, 2 + r)]))
+
+    def rows1(i0, i1):
+        return exact.from_array(np.vstack([gen.rows(kind, m, ns, SEED, 1 + i, 2 + i) for i in picks[i0:i1]]))
+    sec_row1, done1, t1 = _time_dense_pivot(sub, 1, c, rows1, len(picks), budget)
+    sec1 = sec_row1 * (m + 1)
+    out = {"value": 1.0 / sec1, "unit": "pivots/s", "cores": 1, "kind": "port",
+           "sample": (f"oracle/exact.py pivot_dense (the reference's Fraction row operations, "
+                      f"every column) on pivot #1 of {name}, {done1} of {m + 1} rows "
+                      f"({t1:.1f} s on one core), scaled to all rows; host has "
+                      f"{os.cpu_count()} cores"),
+           "seconds_per_pivot": sec1, "seconds_per_pivot_at_1": sec1}
+    if seq and len(seq) > k_mid:
+        # exact state after k_mid pivots of row 0, the pivot rows and a sample
+        prows = sorted({rr for rr, _ in seq[:k_mid + 1]})
+        sample = [i for i in range(0, m, max(1, m // 48)) if i not in set(prows)][:48]
+        keep = prows + sample
+        A = np.vstack([T0] + [gen.rows(kind, m, ns, SEED, 1 + i, 2 + i) for i in keep])
+        X = exact.from_array(A)
+        where = {g: 1 + k for k, g in enumerate(keep)}
+        t0 = time.perf_counter()
+        for rr, cc in seq[:k_mid]:
+            exact.pivot(X, where[rr] - 1, cc)
+        replay = time.perf_counter() - t0
+        rk, ck = seq[k_mid]
+        rows_mid = [X[where[i]] for i in sample if i != rk]
+        sec_row, done, tk = _time_dense_pivot(X, where[rk], ck, lambda i0, i1: rows_mid[i0:i1], len(rows_mid),
+                                              budget)
+        secm = sec_row * (m + 1)
+        out.update({
+            "value": 1.0 / secm, "seconds_per_pivot": secm,
+            "seconds_per_pivot_at_%d" % (k_mid + 1): secm,
+            "sample": out["sample"] + (
+                f"; pivot #{k_mid + 1} (the reported value): the first {k_mid} pivots replayed "
+                f"exactly on row 0, the pivot rows and {len(sample)} sample rows ({replay:.1f} s, "
+                f"not counted), then the same dense pivot on {done} of them ({tk:.1f} s), scaled "
+                f"to all rows -- still a lower bound, denominators keep growing"),
+        })
+    return out
 
 
 def config_table(cpu_budget: float = 20.0) -> None:
@@ -295,7 +350,9 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
     upload(engs, kind, m, ns, spans)
     elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(engs[0], steps, warmup, block, lambda: None, every)
     path, fallbacks = engs[0].exchange_path()
+    geo = engs[0].geometry()
     acc = accounting(steps, block, elapsed, sw_ms, sel_ms, spans[0][1] - spans[0][0] + 1, n)
+    acc["selection_kernel"] = geo["kernel"]
     acc.update(block=block, path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks,
                sweep_avg_us=sw_ms * 1e3, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
                selection_avg_launch_us=sel_ms * 1e3)
@@ -389,11 +446,16 @@ def main():
         eng.set_block(B)
         B = eng.get_block()
         upload([eng], kind, m, ns, [(rb, re_)])
+        xw0 = eng.xwait()
         elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(eng, args.steps, args.warmup, B,
                                                         dist.barrier, args.profile_every)
-        t = torch.tensor([elapsed, sw_ms, sel_ms], dtype=torch.float64)
+        xw1 = eng.xwait()
+        # the cross-rank hop per pivot (block 0: its summary sent -> the
+        # winner's pivot row held), over the timed pivots
+        hop_us = 1e6 * (xw1[0] - xw0[0]) / (xw1[1] - xw0[1]) if xw1[1] > xw0[1] else 0.0
+        t = torch.tensor([elapsed, sw_ms, sel_ms, hop_us], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, sw_ms, sel_ms = float(t[0]), float(t[1]), float(t[2])
+        elapsed, sw_ms, sel_ms, hop_us = float(t[0]), float(t[1]), float(t[2]), float(t[3])
         # distinct GPUs of the job (ranks wrap onto fewer GPUs on a small box)
         ids = [None] * world
         dist.all_gather_object(ids, (os.uname().nodename, device))
@@ -406,7 +468,8 @@ def main():
         sweep_ms = sw_ms
         acc = accounting(args.steps, B, elapsed, sw_ms, sel_ms, local_rows, n)
         acc.update(fallbacks=fallbacks, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
-                   selection_avg_launch_us=sel_ms * 1e3)
+                   selection_avg_launch_us=sel_ms * 1e3, selection_kernel=eng.geometry()["kernel"],
+                   xrank_hop_us_per_pivot=hop_us)
         elapsed_pps = acc["pivots_per_s"]
 
     desc = WORKLOADS[args.workload][3]
@@ -432,9 +495,6 @@ def main():
         "pivots_per_step": B,
         "pivots_timed": acc["pivots"],
         "us_per_pivot": 1e6 / elapsed_pps,
-        # SURVEY §8(d) bytes of one unblocked pivot x pivots/s: the bandwidth an
-        # immediate-update engine would need for this rate
-        "unblocked_equivalent_GBps": pivot_bytes(m, n) * elapsed_pps / 1e9,
         "roofline": {
             "kernel": f"{sweep_kernel(B)} (rank-{B} elimination of {local_rows} local rows)",
             "bound": "hbm",
@@ -442,6 +502,9 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": acc["achieved_GBps"] / HBM_PEAK_GBPS,
+            # the whole pivot: a GPU's sweep bytes per step over the whole
+            # step (selection included) against the same peak
+            "step_frac": acc["sweep_bytes_per_launch"] / (acc["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "traffic": traffic,
             "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch, measured on a build of these "
                              "sources (profiles/r02/hbm_traffic.json, src_sha256)" if traffic else
@@ -456,11 +519,12 @@ def main():
             "f64_peak_TFLOPs": F64_PEAK_TFLOPS,
         },
         "selection": {
-            "kernel": "k_group (persistent pivot selection, latency-bound)",
+            "kernel": f"{acc.get('selection_kernel', 'k_group')} (persistent pivot selection, latency-bound)",
             "us_per_pivot": acc["selection_us_per_pivot"],
             "avg_launch_us": acc["selection_avg_launch_us"],
             "pivots_per_launch": B,
             "time_share": acc["selection_time_share"],
+            **({"xrank_hop_us_per_pivot": acc["xrank_hop_us_per_pivot"]} if world > 1 else {}),
         },
         "fallbacks": acc["fallbacks"],
         "src_sha256": digest,
@@ -476,15 +540,18 @@ def main():
                          "bound": "hbm",
                          "achieved": c3["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": c3["achieved_GBps"] / HBM_PEAK_GBPS,
+                         "step_frac": c3["sweep_bytes_per_launch"] / (c3["ms_per_step"] * 1e-3) / 1e9
+                         / HBM_PEAK_GBPS,
                          "traffic": load_traffic(args.traffic_json, c3["block"], "cfg3", digest),
                          "bytes_per_launch": c3["sweep_bytes_per_launch"],
                          "avg_launch_us": c3["sweep_avg_us"], "time_share": c3["sweep_time_share"]},
-            "selection": {"us_per_pivot": c3["selection_us_per_pivot"],
+            "selection": {"kernel": c3["selection_kernel"], "us_per_pivot": c3["selection_us_per_pivot"],
                           "time_share": c3["selection_time_share"]},
             "path": c3["path"], "fallbacks": c3["fallbacks"],
         }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
+        seq = first_pivots(args.workload, 17, device)
+        out["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds, seq, 16)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -232,6 +232,13 @@ int lp_select_time(lp_handle *h, double *ms, int64_t *launches);
 #define LP_PATH_COLLECTIVE 3
 int lp_exchange_path(const lp_handle *h, int *path, int *fallbacks);
 
+/* Row-sharded persistent selection (LP_PATH_PEER): the cross-rank hop as
+ * this rank's block 0 saw it -- from sending its leaving-row summary (and
+ * speculative pivot row) to holding the winner's pivot row -- summed over
+ * the handle's pivots: *ticks of the 100 MHz device real-time clock over
+ * *pivots pivots (both cumulative since lp_create; read after a call). */
+int lp_xwait(const lp_handle *h, int64_t *ticks, int64_t *pivots);
+
 /* Human-readable description of the last failure on this handle (or of the
  * last failed lp_create* when h is NULL). */
 const char *lp_last_error(const lp_handle *h);

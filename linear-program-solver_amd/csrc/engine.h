@@ -97,6 +97,11 @@ struct Ctl {
     long long g_npiv, g_nstd, g_stuck;
     int g_rule;
     unsigned g_seq;      // the launch (seq) the snapshot belongs to; 0: none
+    // row-sharded persistent selection (XR): block 0's time from sending its
+    // summary to holding the winner's pivot row, summed over the handle's
+    // pivots (100 MHz real-time ticks), and those pivots (lp_xwait)
+    unsigned long long xwait_ticks;
+    long long xwait_pivots;
 };
 
 // Per-block ratio-test summary.
@@ -148,7 +153,11 @@ struct Args {
     int gmaj;            // k_group: granule-major summaries when on one XCD (1, default) or never (0)
     lp_tol tol;
     long long *stamps;   // diagnostic build only (LPGPU_STAMPS=1): k_group phase clocks
-    unsigned long long *gran;  // k_group summaries: 3 regions (ratio, row 0, XCD check) x GROUP_MAXBLOCKS x 8 tagged granules
+    // persistent selections' summaries: GRAN_REGIONS regions of GROUP_MAXBLOCKS x GSLOT (8)
+    // tagged granules -- ratio, row 0, XCD check, and the fourth: k_group's
+    // two-level exchange (8 ratio + 8 row-0 level-2 slots) / k_sel's rescan
+    // and owner answers
+    unsigned long long *gran;
     unsigned spin_max;   // k_group: polls of one exchange before it gives up (timeout)
     unsigned xwait_ms;   // k_group (XR): wall-clock bound of a cross-rank wait
     int fault;           // tests only (LPGPU_FAULT): t + 1 -> block 1 withholds pivot t's ratio summary
@@ -190,6 +199,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
                         hipEvent_t e1 = nullptr);
 
 constexpr int GROUP_MAXBLOCKS = 256;
+constexpr int GRAN_REGIONS = 4;       // regions of Args::gran (see there)
 constexpr int GROUP_MINBLOCKS = 64;    // a small tableau still spreads its columns over 64 blocks
 constexpr int GROUP_THREADS = 64;      // one wave: block reductions stay in registers
 constexpr int GROUP_MAXRPL = 2;        // own rows per lane (<= 64 x 256 x 2 = 32768 rows per device)

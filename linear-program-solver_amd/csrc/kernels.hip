@@ -761,6 +761,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
     for (int k = 0; k < RPL; ++k) ownpiv[k] = 0;
     int stop = 0;                     // block 0: the objective increased (simplex.py:133)
     int ndone = 0;                    // pivots of this launch completed (their M in lM)
+    unsigned long long xwait = 0;     // XR: cross-rank waits of this block (Ctl::xwait_ticks)
     for (int tv = 0; tv < count; ++tv) {
         // the pivot index is wave-uniform; saying so keeps the chains'
         // trip counts and bounds in SGPRs (scalar branches, no exec masking:
@@ -1191,6 +1192,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 send_row(3);
             }
             unsigned x[7];
+            const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
             if (!gather_x<7>(xs, N, gtag(seq, t, 2), x, &ctl->bar_timeout, xticks)) {
                 status = LP_DEVICE_ERROR;
                 break;
@@ -1301,6 +1303,7 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
                 }
                 if (status != LP_PIVOTED) break;
             }
+            xwait += __builtin_amdgcn_s_memrealtime() - xw0;
         } else {
             prow(R, 0.0);
         }
@@ -1438,6 +1441,10 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
             const int s = (int)(e % (4 * BMAX) >> 2);
             if (row >= lr0 && row < lr1 && s < nds) *gp(&A.MQ[e]) = lM[(row - lr0) * cs + s];
         }
+    }
+    if (XR && b == 0 && tid == 0) {
+        *gp(&ctl->xwait_ticks) += xwait;
+        *gp(&ctl->xwait_pivots) += ndone;
     }
     if (b == 0 && tid == 0) {
         // an increase at the launch's last pivot: nothing read the flag yet
@@ -2287,8 +2294,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         long long ld = ap->ld, rows = ap->rows;
         int grpv = grp, nsv = (int)nsg;
         void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail};
-        (void)hipExtLaunchKernel(fn, grid, dim3(64 * wv), args, 0, s, e0, e1, 0);
-        return hipGetLastError();
+        const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * wv), args, 0, s, e0, e1, 0);
+        return err != hipSuccess ? err : hipGetLastError();
     }
     const int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
     long long nrun = (long long)sweep_cus() * bpc / ns;

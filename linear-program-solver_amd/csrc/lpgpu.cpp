@@ -411,7 +411,7 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMemsetAsync(h->MQ, 0, mqbytes, h->s));
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
-    const size_t gbytes = 4 * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);   // k_group summary regions
+    const size_t gbytes = lpk::GRAN_REGIONS * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
     HCHK(h, hipMalloc(&h->gran, gbytes));
     HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
     HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));
@@ -1110,7 +1110,11 @@ static int recover_timeout(const Members &M, const std::vector<Args> &A, int mod
     for (size_t k = 0; k < M.size(); ++k) {
         lp_handle *h = M[k];
         Ctl c = *h->hctl;
+        // the handle stays on the per-pivot kernels from here on (a timeout
+        // is never expected; lp_exchange_path reports it as a fallback), and
+        // its automatic pivots per sweep is re-chosen for those kernels
         h->persistent = false;
+        h->block_auto = 0;
         h->fallbacks += 1;
         h->eager_ok = false;
         HCHK(h, lpk::launch_load_eager(h->s, A[k]));
@@ -1594,6 +1598,13 @@ extern "C" int lp_form_checks(lp_handle *h, int32_t *flags, int64_t *bcols)
     flags[2] = unbounded;
     flags[3] = infeasible;                                  // :510-514
     flags[4] = cs[0].nnz < h->m;                            // :516-518: some b_i == 0
+    return LP_PIVOTED;
+}
+
+extern "C" int lp_xwait(const lp_handle *h, int64_t *ticks, int64_t *pivots)
+{
+    *ticks = (int64_t)h->hctl->xwait_ticks;
+    *pivots = h->hctl->xwait_pivots;
     return LP_PIVOTED;
 }
 

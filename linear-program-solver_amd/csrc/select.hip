@@ -46,8 +46,32 @@
 namespace lpk {
 namespace {
 
+// diagnostic build only (-DLPK_STAMPS, LPGPU_STAMPS=1): per-phase shader-
+// cycle sums kept in scalar registers for the whole launch and stored once
+// at its end (scripts/sel_clocks.py) -- no memory traffic in the loop
+#ifdef LPK_STAMPS
+// (the sums are 32-bit and kept in VGPRs -- in SGPRs they pushed the kernel
+// into spilling scalar registers, which distorted what they measured)
+#define SEL_CLK_DECL unsigned clk_[16] = {}; unsigned long long clk_t = __builtin_amdgcn_s_memtime(), clk_r0 = 0;
+#define SEL_CLK(k)                                                                \
+    do {                                                                          \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();               \
+        clk_[k] = vgpr(clk_[k] + (unsigned)(n_ - clk_t));                         \
+        clk_t = n_;                                                               \
+    } while (0)
+#define SEL_DONE(x)                                                               \
+    do {                                                                          \
+        const int z_ = __builtin_amdgcn_readfirstlane((int)__double_as_longlong(x)); \
+        asm volatile("s_nop 0" ::"s"(z_));                                        \
+    } while (0)
+#else
+#define SEL_CLK_DECL
+#define SEL_CLK(k) do {} while (0)
+#define SEL_DONE(x) do {} while (0)
+#endif
+
 constexpr int SEL_NGR = 7;   // ratio summary: l (2), i, a (2), b (2)
-constexpr int SEL_NGE = 6;   // row-0 summary: l (2), q (2), i, fneg
+constexpr int SEL_NGE = 8;   // row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
 constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
 typedef double d16 __attribute__((ext_vector_type(16)));
 
@@ -187,6 +211,17 @@ __device__ __forceinline__ void row_chain(double (&x)[IPL], const double (&mr)[N
 // immediate offset (the per-granule addresses of the general layout, kept
 // live across the pivot loop, cost k_sel about 70 VGPRs).
 constexpr int SEL_SLOT = 64;
+// a loop-invariant operand moved into a VGPR (the asm makes it look
+// divergent, so it stays there): k_sel keeps its kernel arguments, per-block
+// constants and tolerances in VGPRs -- in SGPRs the compiler ran out (106)
+// and spilled about 70 of them into VGPR lanes, a v_readlane per use
+template <typename T>
+__device__ __forceinline__ T vgpr(T x)
+{
+    asm("" : "+v"(x));
+    return x;
+}
+
 // the words of a summary: lane g (< n) stores word g of block b
 __device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, unsigned w, int n, bool fast)
 {
@@ -217,6 +252,79 @@ __device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (
     }
 }
 
+
+// row-0 summary of a block's own columns (columns j = jc0 + lane + 64 k; vv =
+// INFINITY where j is not one of them): slice minimum el, first column within
+// the tie band of el (ei, its value eq, and P[t][ei] = epc from pv), first
+// column with c_j < -tol.cost (efn)
+template <int IPL>
+__device__ __forceinline__ void sel_summary(const double (&vv)[IPL], const double (&pv)[IPL], double vmin,
+                                            long long jc0, const lp_tol &tol, double &el, long long &ei,
+                                            double &eq, double &epc, long long &efn)
+{
+    el = wave_min(vmin);
+    efn = NONE;
+    ei = NONE;
+    eq = 0.0;
+    epc = 0.0;
+    const double ethr = tie_band(el, tol.cost_tie);
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) {
+        const u64 mn = __ballot(vv[k] < -tol.cost);
+        if (mn && efn == NONE) efn = jc0 + k * 64 + __builtin_ctzll(mn);
+        const u64 mb = __ballot(el < INFINITY && vv[k] <= ethr);
+        if (mb && ei == NONE) {
+            const int f = __builtin_ctzll(mb);
+            ei = jc0 + k * 64 + f;
+            eq = rl_d(lo32(vv[k]), hi32(vv[k]), f);
+            epc = rl_d(lo32(pv[k]), hi32(pv[k]), f);
+        }
+    }
+}
+// this lane's word of a row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
+__device__ __forceinline__ unsigned esum_word(double el, double eq, long long ei, long long efn, double epc)
+{
+    const int lane = threadIdx.x;
+    return lane == 0 ? lo32(el) : lane == 1 ? hi32(el) : lane == 2 ? lo32(eq) : lane == 3 ? hi32(eq)
+         : lane == 4 ? idx32(ei) : lane == 5 ? idx32(efn) : lane == 6 ? lo32(epc) : hi32(epc);
+}
+// sel_gather split in two: issue() sends the first polls, finish() checks them
+// (and polls on); work placed between the two runs while the polls are in
+// flight (the scheduling barriers keep the loads ahead of it)
+template <int NG>
+struct SelPoll {
+    const u64 *p;
+    u64 v[NG];
+    __device__ __forceinline__ void issue(const u64 *base, unsigned G)
+    {
+        p = base + min((unsigned)threadIdx.x, G - 1);
+#pragma unroll
+        for (int g = 0; g < NG; ++g) v[g] = ld_sc1(p + g * SEL_SLOT);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __device__ __forceinline__ bool finish(unsigned tag, unsigned (&w)[NG], unsigned *timeout_flag,
+                                           unsigned spin_max)
+    {
+        __builtin_amdgcn_sched_barrier(0);
+        for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                w[g] = (unsigned)v[g];
+                ok = ok && (unsigned)(v[g] >> 32) == tag;
+            }
+            if (__all(ok)) return true;
+            if (spins > spin_max) {
+                st_sc1(timeout_flag, 1u);
+                return false;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) v[g] = ld_sc1(p + g * SEL_SLOT);
+        }
+    }
+};
+
 }  // namespace
 
 // NB: most pivots of a launch (register multipliers); IPL: own columns per
@@ -237,7 +345,6 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     extern __shared__ __attribute__((aligned(16))) double lP[];   // [cpb][CS]: P[s][own column]
     const unsigned b = blockIdx.x >> 3, G = (unsigned)gper;
     const int lane = threadIdx.x;
-    const Args &Ar = A;
     Ctl *ctl = A.ctl;
     const bool reset = (first & 1) != 0, eager = (first & 2) != 0, enter = (first & 4) != 0;
     if (b == 0 && lane == 0) *gp(&ctl->ndef[grp]) = 0;
@@ -260,15 +367,31 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         st_sc1(&ctl->g_rule, rule);
         st_sc1(&ctl->g_seq, seq);
     }
-    const long long ld = A.ld;
+    // loop-invariant operands in VGPRs (vgpr())
+    const long long ld = vgpr(A.ld);
+    double *const Tv = vgpr(A.T);
+    double *const Pv = vgpr(A.P);
+    double *const Mv = vgpr(A.M);
+    double *const MQv = vgpr(A.MQ);
+    double *const row0v = vgpr(A.row0);
+    double *const col0v = vgpr(A.col0);
+    const long long rowsv = vgpr(A.rows);
+    const long long nv = vgpr(A.n);
+    lp_tol tol;
+    tol.cost = vgpr(A.tol.cost);
+    tol.cost_tie = vgpr(A.tol.cost_tie);
+    tol.pivot = vgpr(A.tol.pivot);
+    tol.zero = vgpr(A.tol.zero);
+    tol.ratio_tie = vgpr(A.tol.ratio_tie);
+    tol.stall = vgpr(A.tol.stall);
     // own rows: lane l holds row lr0 + l; own columns: j = jc0 + l + 64 k, a
     // block's share of the variable columns 1..n (column 0 is every block's)
     const long long rpb = (A.rc + G - 1) / G;
-    const long long lr0 = 1 + (long long)b * rpb, lr1 = min(lr0 + rpb, A.rows);
+    const long long lr0 = vgpr(1 + (long long)b * rpb), lr1 = vgpr(min(1 + (long long)b * rpb + rpb, A.rows));
     const long long li = lr0 + lane;
     const bool own = li < lr1;
     const long long cpb = (A.n + G - 1) / G;
-    const long long jc0 = 1 + (long long)b * cpb, jc1 = min(jc0 + cpb, A.n + 1);
+    const long long jc0 = vgpr(1 + (long long)b * cpb), jc1 = vgpr(min(1 + (long long)b * cpb + cpb, A.n + 1));
     int jk[IPL];
     bool cok[IPL];
     int kc[IPL];
@@ -282,23 +405,33 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     // eager copies, or (first launch after an upload) the stored tableau's
     double l0v[IPL];
 #pragma unroll
-    for (int k = 0; k < IPL; ++k) l0v[k] = cok[k] ? (eager ? *gp(A.T + jk[k]) : *gp(A.row0 + jk[k])) : 0.0;
-    double v0 = eager ? *gp(A.T) : *gp(A.row0);
-    double lcv = own ? (eager ? *gp(A.T + li * ld) : *gp(A.col0 + li)) : 0.0;
+    for (int k = 0; k < IPL; ++k) l0v[k] = cok[k] ? (eager ? *gp(Tv + jk[k]) : *gp(row0v + jk[k])) : 0.0;
+    double v0 = eager ? *gp(Tv) : *gp(row0v);
+    double lcv = own ? (eager ? *gp(Tv + li * ld) : *gp(col0v + li)) : 0.0;
     if (eager) {
         // the other blocks read row0[C] (a pivot's row-0 multiplier)
 #pragma unroll
         for (int k = 0; k < IPL; ++k)
-            if (cok[k]) st_sc1(&A.row0[jk[k]], l0v[k]);
+            if (cok[k]) st_sc1(&row0v[jk[k]], l0v[k]);
     }
     // LDS pivot values start at zero: the chains' padding pivots multiply them by 0
     for (long long e = lane; e < (cpb * CS + 8) / 2; e += GROUP_THREADS)
         reinterpret_cast<double2 *>(lP)[e] = make_double2(0.0, 0.0);
     // summary regions: ratio, row 0, XCD check, rescan answers
-    u64 *grR = A.gran;
-    u64 *grE = A.gran + GROUP_MAXBLOCKS * GSLOT;
-    u64 *grX = A.gran + 2 * GROUP_MAXBLOCKS * GSLOT;
-    u64 *grS = A.gran + 3 * GROUP_MAXBLOCKS * GSLOT;
+    u64 *const grR = vgpr(A.gran);
+    u64 *const grE = vgpr(A.gran + GROUP_MAXBLOCKS * GSLOT);
+    u64 *const grX = vgpr(A.gran + 2 * GROUP_MAXBLOCKS * GSLOT);
+    u64 *const grS = vgpr(A.gran + 3 * GROUP_MAXBLOCKS * GSLOT);
+    ERec *const erecv = vgpr(A.erec);
+    long long *const logv = vgpr(A.log);
+    long long *const dRv = vgpr(A.dR);
+    long long *const dCv = vgpr(A.dC);
+    const long long logcapv = vgpr(A.logcap);
+    const unsigned spinv = vgpr(A.spin_max);
+    Ctl *const ctlv = vgpr(ctl);            // the loop's hand-off flags and records
+    u64 *const xbufv = vgpr(A.xbuf);        // XR: this rank's exchange buffer, the peers'
+    unsigned long long *const *const peerv = vgpr(A.peer);
+    const long long rbv = vgpr(A.rb);
     bool fast = false;
     {
         // every block publishes its XCD; plain (L2-resident) hand-off stores
@@ -308,7 +441,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         drain_stores();
         if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | xcc);
         unsigned wx[1];
-        if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
+        if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctlv->bar_timeout, spinv)) {
             if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
             return;
         }
@@ -344,53 +477,46 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     int status = LP_PIVOTED;
     int stop = 0;                               // the objective increased (simplex.py:133)
     int ndone = 0;
-    for (int tv = 0; tv < count; ++tv) {
-        const int t = __builtin_amdgcn_readfirstlane(tv);
-        stamp(Ar, b, t, 0);
-        // ---- entering column
-        long long C;
-        if (t == 0 && !from_erec && !enter) {
+    unsigned long long xwait = 0;              // XR: block 0's cross-rank waits (Ctl::xwait_ticks)
+    SEL_CLK_DECL
+    // ---- the first pivot's entering column (call start: every block's
+    //      summary of its row-0 slice; later launches: the previous launch's
+    //      records; or given).  Row 0 in memory is current here (kernel
+    //      boundary, or stored write-through above), so f0 and rare rescans
+    //      read it directly.
+    long long C = NONE;
+    double f0 = 0.0, pcw = 0.0;               // row 0 at C; P[t - 1][C] (t > 0, from the summaries)
+    {
+        const bool capped = cap >= 0 && npiv >= cap;
+        if (!from_erec && !enter) {
             C = ld_sc1(&ctl->c) + 1;
         } else {
-            const bool capped = cap >= 0 && npiv >= cap;
             double el = INFINITY, eq = 0.0;
             long long ei = NONE, ef = NONE;
             const bool in = (unsigned)lane < G;
-            if (t == 0 && from_erec) {          // previous launch's summaries (kernel boundary)
+            if (from_erec) {
                 if (in) {
-                    el = ld_sc1(&A.erec[lane].l);
-                    ei = ld_sc1(&A.erec[lane].i);
-                    eq = ld_sc1(&A.erec[lane].q);
-                    ef = ld_sc1(&A.erec[lane].fneg);
+                    el = ld_sc1(&erecv[lane].l);
+                    ei = ld_sc1(&erecv[lane].i);
+                    eq = ld_sc1(&erecv[lane].q);
+                    ef = ld_sc1(&erecv[lane].fneg);
                 }
             } else {
-                const unsigned etag = t == 0 ? gtag(seq, 0, 0) : gtag(seq, t - 1, 1);
-                if (t == 0) {
-                    // first pivot of a call: every block's summary of its row-0 slice
-                    double vv[IPL], vmin = INFINITY;
+                double vv[IPL], vmin = INFINITY, pz[IPL];
 #pragma unroll
-                    for (int k = 0; k < IPL; ++k) {
-                        vv[k] = cok[k] ? l0v[k] : INFINITY;
-                        vmin = fmin(vmin, vv[k]);
-                    }
-                    double sel_, seq_;
-                    long long sei_, sfn_;
-                    row0_summary<IPL>(vv, vmin, jc0, A.tol, sel_, sei_, seq_, sfn_);
-                    unsigned wv = 0;
-                    if (lane == 0) wv = lo32(sel_);
-                    else if (lane == 1) wv = hi32(sel_);
-                    else if (lane == 2) wv = lo32(seq_);
-                    else if (lane == 3) wv = hi32(seq_);
-                    else if (lane == 4) wv = idx32(sei_);
-                    else if (lane == 5) wv = idx32(sfn_);
-                    drain_stores();
-                    sel_put(grE, b, etag, wv, SEL_NGE, fast);
+                for (int k = 0; k < IPL; ++k) {
+                    vv[k] = cok[k] ? l0v[k] : INFINITY;
+                    vmin = fmin(vmin, vv[k]);
+                    pz[k] = 0.0;
                 }
+                double sel_, seq_, spc_;
+                long long sei_, sfn_;
+                sel_summary<IPL>(vv, pz, vmin, jc0, tol, sel_, sei_, seq_, spc_, sfn_);
+                const unsigned etag = gtag(seq, 0, 0);
+                drain_stores();
+                sel_put(grE, b, etag, esum_word(sel_, seq_, sei_, sfn_, spc_), SEL_NGE, fast);
                 unsigned w[SEL_NGE];
-                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctl->bar_timeout, A.spin_max)) {
-                    status = LP_DEVICE_ERROR;
-                    break;
-                }
+                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctlv->bar_timeout, spinv)) status = LP_DEVICE_ERROR;
                 if (in) {
                     el = mk_d(w[0], w[1]);
                     eq = mk_d(w[2], w[3]);
@@ -398,16 +524,14 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     ef = un_idx(w[5]);
                 }
             }
-            if (stop || capped) {
+            if (capped) {
                 C = NONE;
             } else if (rule == LP_RULE_MIN_INDEX) {
                 C = wave_min_ll(ef);
             } else {
                 const double g = wave_min(el);
-                if (!(g < -A.tol.cost)) {
-                    C = NONE;
-                } else {
-                    const double ethr = tie_band(g, A.tol.cost_tie);
+                if (g < -tol.cost) {
+                    const double ethr = tie_band(g, tol.cost_tie);
                     double l1[1] = {el}, q1[1] = {eq};
                     long long i1[1] = {ei};
                     C = combine_loaded<1>(l1, i1, q1, G, ethr);
@@ -415,62 +539,67 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                         const long long k0 = 1 + (-1 - C) * cpb, k1 = min(k0 + cpb, A.n + 1);
                         long long best = NONE;
                         for (long long k = k0 + lane; k < k1; k += GROUP_THREADS)
-                            if (ld_sc1(&A.row0[k]) <= ethr) { best = k; break; }
+                            if (ld_sc1(&row0v[k]) <= ethr) { best = k; break; }
                         C = wave_min_ll(best);
                     }
                 }
             }
-            if (C == NONE) status = stop ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
+            if (C == NONE && status == LP_PIVOTED) status = capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
-        stamp(Ar, b, t, 1);
-        bstamp(Ar, b, t, 2);
-        if (status != LP_PIVOTED) break;
+        if (C != NONE) f0 = ld_sc1(&row0v[C]);
+    }
+    for (int tv = 0; tv < count && status == LP_PIVOTED; ++tv) {
+        const int t = __builtin_amdgcn_readfirstlane(tv);
+        if (t == 0) {
+            SEL_CLK(15);                      // the launch's start, not a pivot's phase
+#ifdef LPK_STAMPS
+            clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+        }
         // ---- one round trip: the own rows' elements of column C (a pivot row
-        //      of this launch: P[pstar][C]), P[s][C] of the earlier pivots for
-        //      the broadcasts, row 0's value at C
+        //      of this launch: P[pstar][C]) and P[s][C] of the earlier pivots
+        //      for the broadcasts; P[t - 1][C] came with the summaries
         // (every load unconditional and the selects after the last one: a
         // select right after its load made the compiler wait for each load
         // in turn -- four round trips instead of one)
-        const double *ap = pstar >= 0 ? A.P + (long long)pstar * ld : A.T + (own ? li : 0) * ld;
+        const double *ap = pstar >= 0 ? Pv + (long long)pstar * ld : Tv + (own ? li : 0) * ld;
         double a = ld_sc1(ap + C);
         double pk[NK];
 #pragma unroll
         for (int k = 0; k < NK; ++k)
-            pk[k] = ld_sc1(&A.P[(long long)max(min(16 * k + (lane & 15), t - 1), 0) * ld + C]);
-        const double f0 = ld_sc1(&A.row0[C]);
-        a = own ? a : 0.0;
+            pk[k] = ld_sc1(&Pv[(long long)max(min(16 * k + (lane & 15), t - 2), 0) * ld + C]);
+        a = own ? (pstar >= 0 && pstar == t - 1 ? pcw : a) : 0.0;
 #pragma unroll
-        for (int k = 0; k < NK; ++k) pk[k] = 16 * k + (lane & 15) < t ? pk[k] : 0.0;
-        if (b == 0 && lane == 0) st_x(&ctl->c, C - 1, fast);
-        stamp(Ar, b, t, 2);
-        if (STAMPS && A.stamps) {   // diagnostic: the column elements have arrived
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            bstamp(Ar, b, t, 3);
-            stamp(Ar, b, t, 3);
+        for (int k = 0; k < NK; ++k) {
+            const int sk = 16 * k + (lane & 15);
+            pk[k] = sk < t - 1 ? pk[k] : sk == t - 1 ? pcw : 0.0;
         }
+        SEL_CLK(1);
+        if (STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: the column has arrived
+        SEL_CLK(2);
         col_chain<NK>(a, pk, m0, m1, m2, m3, t);
-        // M[t] of the own rows: read by later pivots' row chains (drained with
-        // this pivot's row-0 publication, not with the ratio summary)
-        if (own) st_x(&A.M[mi(A.rows, li, t)], a, fast);
-        if (b == 0 && lane == 0) {            // row 0's multiplier (+ the sweep's copy)
-            st_x(&A.M[mi(A.rows, 0, t)], f0, fast);
-            *gp(&A.MQ[mq(0, t)]) = f0;
-        }
+        SEL_DONE(a);
+        SEL_CLK(3);
         // ---- ratio test over the own rows
         bool okq;
-        const double q = row_ratio(a, lcv, A.tol, okq);
+        const double q = row_ratio(a, lcv, tol, okq);
         okq = okq && own;
         const double lb = wave_min(okq ? q : INFINITY);
         long long ib = NONE;
         double ab = 0.0, bb = 0.0;
         if (lb < INFINITY) {
-            const u64 mask = __ballot(okq && q <= tie_band(lb, A.tol.ratio_tie));
+            const u64 mask = __ballot(okq && q <= tie_band(lb, tol.ratio_tie));
             const int f = __builtin_ctzll(mask);
             ib = lr0 + f;
             ab = rl_d(lo32(a), hi32(a), f);
             bb = rl_d(lo32(lcv), hi32(lcv), f);
         }
-        stamp(Ar, b, t, 4);
+        SEL_DONE(lb);
+        SEL_CLK(4);
+        // the drain makes the previous pivot's P stores visible with this
+        // summary (read from pivot t + 1 on); this pivot's multipliers are
+        // stored after it and drained with the next one
+        drain_stores();
         if (!(A.fault == t + 1 && b == min(1u, G - 1))) {   // fault injection (tests): block 1 (0) never publishes
             unsigned wv = idx32(ib);
             if (lane == 0) wv = lo32(lb);
@@ -481,9 +610,18 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             else if (lane == 6) wv = hi32(bb);
             sel_put(grR, b, gtag(seq, t, 0), wv, SEL_NGR, fast);
         }
-        bstamp(Ar, b, t, 0);
-        stamp(Ar, b, t, 5);
-        // the multiplier into its register while the summaries travel
+        SEL_CLK(5);
+        // ---- leaving row: the polls go out first, then (while the summaries
+        //      travel) the multiplier into its register and to memory
+        unsigned w[SEL_NGR];
+        SelPoll<SEL_NGR> pr;
+        pr.issue(grR, G);
+        if (own) st_x(&Mv[mi(rowsv, li, t)], a, fast);
+        if (b == 0 && lane == 0) {            // read after the launch only (after the publication:
+            *gp(&ctlv->c) = C - 1;            // stores pending at a drain delay the summary)
+            *gp(&Mv[mi(rowsv, 0, t)]) = f0;   // row 0's multiplier (+ the sweep's copy)
+            *gp(&MQv[mq(0, t)]) = f0;
+        }
         {
             const int u = t & 15;
             switch (t >> 4) {
@@ -493,25 +631,22 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             default: if constexpr (NK > 3) m3[u] = a; break;
             }
         }
-
-        // ---- leaving row (combine the ratio summaries)
-        unsigned w[SEL_NGR];
-        if (!sel_gather<SEL_NGR>(grR, G, gtag(seq, t, 0), w, &ctl->bar_timeout, A.spin_max)) {
+        if (!pr.finish(gtag(seq, t, 0), w, &ctlv->bar_timeout, spinv)) {
             status = LP_DEVICE_ERROR;
             break;
         }
-        stamp(Ar, b, t, 6);
+        SEL_CLK(6);
         const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
         const double g = wave_min(rl);
         long long R = NONE;                   // this device's leaving row (XR: its candidate)
         double aR = 0.0, bR = 0.0;
         if (g < INFINITY) {
-            const double thr = tie_band(g, A.tol.ratio_tie);
+            const double thr = tie_band(g, tol.ratio_tie);
             const int bs = __builtin_ctzll(__ballot((unsigned)lane < G && rl <= thr));
             aR = rl_d(w[3], w[4], bs);
             bR = rl_d(w[5], w[6], bs);
             bool okr;
-            const double qr = row_ratio(aR, bR, A.tol, okr);
+            const double qr = row_ratio(aR, bR, tol, okr);
             if (okr && qr <= thr) {
                 R = un_idx(rl32(w[2], bs));
             } else {
@@ -530,7 +665,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     sel_put(grS, 0, stag, wv, SEL_NGS, fast);
                 }
                 unsigned y[SEL_NGS];
-                if (!sel_gather<SEL_NGS>(grS, 1, stag, y, &ctl->bar_timeout, A.spin_max)) {
+                if (!sel_gather<SEL_NGS>(grS, 1, stag, y, &ctlv->bar_timeout, spinv)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -542,7 +677,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             status = LP_UNBOUNDED;
             break;
         }
-        stamp(Ar, b, t, 7);
+        SEL_CLK(7);
         // ---- pivot row on the own columns: prow(Rl, av) = current values of
         //      local row Rl (stored row, or P[s*] if it was pivot row s* of
         //      this launch, + the later pivots of the launch) / av
@@ -553,11 +688,11 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             // every load issued before any select (see the column's)
             double x[IPL];
 #pragma unroll
-            for (int k = 0; k < IPL; ++k) x[k] = *gp(A.T + Rl * ld + min(jk[k], (int)A.n));
+            for (int k = 0; k < IPL; ++k) x[k] = *gp(Tv + Rl * ld + min(jk[k], (int)nv));
             double mr[NK];
 #pragma unroll
             for (int k = 0; k < NK; ++k)
-                mr[k] = ld_sc1(&A.M[mi(A.rows, Rl, max(min(16 * k + (lane & 15), t - 1), 0))]);
+                mr[k] = ld_sc1(&Mv[mi(rowsv, Rl, max(min(16 * k + (lane & 15), t - 1), 0))]);
 #pragma unroll
             for (int k = 0; k < IPL; ++k) x[k] = sst >= 0 ? lP[kc[k] * CS + sst] : (cok[k] ? x[k] : 0.0);
 #pragma unroll
@@ -565,33 +700,27 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 const int s = 16 * k + (lane & 15);
                 mr[k] = (s < t && s > sst) ? mr[k] : 0.0;
             }
-            if (STAMPS && A.stamps) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                stamp(Ar, b, t, 8);
-            }
+            if (STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: the row has arrived
+            SEL_CLK(8);
             row_chain<IPL, NB>(x, mr, lP, kc, t);
-            if (STAMPS && A.stamps) {
-                asm volatile("" ::"v"(x[0]), "v"(x[IPL - 1]));
-                stamp(Ar, b, t, 12);
-            }
+            SEL_DONE(x[IPL - 1]);
+            SEL_CLK(9);
 #pragma unroll
             for (int k = 0; k < IPL; ++k) pv[k] = (jk[k] == C) ? 1.0 : x[k] / avv;
-            if (STAMPS && A.stamps) {
-                asm volatile("" ::"v"(pv[0]), "v"(pv[IPL - 1]));
-                stamp(Ar, b, t, 13);
-            }
+            SEL_DONE(pv[IPL - 1]);
+            SEL_CLK(10);
         };
         bool win = true;                      // this rank holds the leaving row
-        long long rglob = R == NONE ? -1 : R - 1 + A.rb;
+        long long rglob = R == NONE ? -1 : R - 1 + rbv;
         if constexpr (XR) {
             // ---- leaving row across ranks (as k_group): every rank sends
             //      (local minimum, global row, pivot element, b) to all ranks
             //      and, without waiting for the verdict, its candidate's
             //      normalised row on every block's columns
             const int par = t & 1;
-            const int N = A.nranks;
+            const int N = A.nranks;                 // (a uniform loop bound: kept scalar)
             const unsigned long long xticks = (unsigned long long)A.xwait_ms * 100000ull;
-            u64 *xsl = A.xbuf + par * XS_SUM_PAR;
+            u64 *xsl = xbufv + par * XS_SUM_PAR;
             if (b == 0 && lane < SEL_NGR) {
                 const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
                 unsigned wv = 0;
@@ -603,13 +732,13 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 else if (lane == 5) wv = lo32(bR);
                 else wv = hi32(bR);
                 for (int p = 0; p < N; ++p)
-                    st_sys(&(*gp(A.peer + p))[par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
+                    st_sys(&(*gp(peerv + p))[par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
             }
             auto send_row = [&](int ph) {
                 const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
                 for (int p = 0; p < N; ++p) {
                     if (p == A.rank) continue;
-                    u64 *dst = (*gp(A.peer + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
+                    u64 *dst = (*gp(peerv + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
                                (long long)b * XS_PROW_BLOCK;
 #pragma unroll
                     for (int k = 0; k < IPL; ++k) {
@@ -626,7 +755,8 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 send_row(3);
             }
             unsigned x[SEL_NGR];
-            if (!gather_x<SEL_NGR>(xsl, N, gtag(seq, t, 2), x, &ctl->bar_timeout, xticks)) {
+            const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
+            if (!gather_x<SEL_NGR>(xsl, N, gtag(seq, t, 2), x, &ctlv->bar_timeout, xticks)) {
                 status = LP_DEVICE_ERROR;
                 break;
             }
@@ -636,11 +766,11 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 status = LP_UNBOUNDED;
                 break;
             }
-            const double thr = tie_band(gg, A.tol.ratio_tie);
+            const double thr = tie_band(gg, tol.ratio_tie);
             const int ps = __builtin_ctzll(__ballot(lane < N && lp <= thr));
             double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
             bool okp;
-            const double qs = row_ratio(as, bs, A.tol, okp);
+            const double qs = row_ratio(as, bs, tol, okp);
             long long rg;
             int ph = 3;                       // the tag of the winner's row slices
             if (okp && qs <= thr) {
@@ -654,7 +784,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     const u64 mk = __ballot(okq && q <= thr);
                     const int fr = mk ? __builtin_ctzll(mk) : 0;
                     const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
-                    u64 *loc = A.xbuf + XS_PROW + 2LL * N * XS_PROW_RANK;
+                    u64 *loc = xbufv + XS_PROW + 2LL * N * XS_PROW_RANK;
                     if (lane < SEL_NGS) {
                         const unsigned wv = lane == 0 ? (mk ? (unsigned)(lr0 + fr) : 0x7fffffffu)
                                           : lane == 1 ? lo32(ar) : lane == 2 ? hi32(ar)
@@ -662,7 +792,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                         st_sc1(&loc[b * 8 + lane], ((u64)gtag(seq, t, 4) << 32) | wv);
                     }
                     unsigned wl[1][SEL_NGS];
-                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wl, &ctl->bar_timeout, A.spin_max)) {
+                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wl, &ctlv->bar_timeout, spinv)) {
                         status = LP_DEVICE_ERROR;
                         break;
                     }
@@ -670,15 +800,15 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     const unsigned r0w = rl32(wl[0][0], bf), a0 = rl32(wl[0][1], bf), a1 = rl32(wl[0][2], bf),
                                    b0 = rl32(wl[0][3], bf), b1 = rl32(wl[0][4], bf);
                     if (b == 0 && lane < SEL_NGS) {
-                        const unsigned wv = lane == 0 ? (unsigned)((long long)r0w - 1 + A.rb)
+                        const unsigned wv = lane == 0 ? (unsigned)((long long)r0w - 1 + rbv)
                                           : lane == 1 ? a0 : lane == 2 ? a1 : lane == 3 ? b0 : b1;
                         for (int p = 0; p < N; ++p)
-                            st_sys(&(*gp(A.peer + p))[par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
+                            st_sys(&(*gp(peerv + p))[par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
                                    ((u64)gtag(seq, t, 5) << 32) | wv);
                     }
                 }
                 unsigned y[SEL_NGS];
-                if (!gather_x<SEL_NGS>(xsl + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctl->bar_timeout, xticks)) {
+                if (!gather_x<SEL_NGS>(xsl + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctlv->bar_timeout, xticks)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -687,18 +817,18 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 bs = mk_d(__builtin_amdgcn_readfirstlane(y[3]), __builtin_amdgcn_readfirstlane(y[4]));
                 ph = 6;
                 if (A.rank == ps) {
-                    prow(rg - A.rb + 1, as);
+                    prow(rg - rbv + 1, as);
                     send_row(6);
                 }
             }
             win = A.rank == ps;
             rglob = rg;
-            R = win ? rg - A.rb + 1 : -1;
+            R = win ? rg - rbv + 1 : -1;
             aR = as;
             bR = bs;
             if (!win) {
                 // the winning rank's block b sent these columns
-                const u64 *src = A.xbuf + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
+                const u64 *src = xbufv + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
                                  (long long)b * XS_PROW_BLOCK;
                 const unsigned tg = gtag(seq, t, ph);
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -713,7 +843,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     }
                     if (__all(ok)) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
-                        st_sc1(&ctl->bar_timeout, 1u);
+                        st_sc1(&ctlv->bar_timeout, 1u);
                         status = LP_DEVICE_ERROR;
                         break;
                     }
@@ -721,14 +851,19 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 }
                 if (status != LP_PIVOTED) break;
             }
+            xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
         } else {
             prow(R, aR);
         }
-        // ---- P[t], row 0 and column 0 (every block: p0 = b / a)
+        // ---- P[t], row 0 and column 0 (every block: p0 = b / a).  P[t] is
+        //      read from pivot t + 2 on (drained with pivot t + 1's ratio
+        //      summary; pivot t + 1 gets P[t][C] with the row-0 summaries);
+        //      row 0 is stored once, at the end of the launch
         const double p0 = bR / aR;
 #pragma unroll
         for (int k = 0; k < IPL; ++k)
-            if (cok[k]) st_x(&A.P[t * ld + jk[k]], pv[k], fast);
+            if (cok[k]) st_x(&Pv[t * ld + jk[k]], pv[k], fast);
+        if (b == 0 && lane == 0) *gp(&Pv[t * ld]) = p0;   // read after the launch (sweep)
         double vn[IPL], vv[IPL], vmin = INFINITY;
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
@@ -736,97 +871,197 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             vv[k] = cok[k] ? vn[k] : INFINITY;
             vmin = fmin(vmin, vv[k]);
         }
-#pragma unroll
-        for (int k = 0; k < IPL; ++k)
-            if (cok[k]) st_x(&A.row0[jk[k]], vn[k], fast);
-        if (b == 0 && lane == 0) *gp(&A.P[t * ld]) = p0;   // read after the launch (sweep)
-#pragma unroll
-        for (int k = 0; k < IPL; ++k) {
-            if (cok[k]) lP[kc[k] * CS + t] = pv[k];
-            l0v[k] = vn[k];
-        }
         v0 = upd(0, -1, f0, p0, v0);
-        stamp(Ar, b, t, 9);
-        double el, eq;
+        double el, eq, epc;
         long long ei, efn;
-        row0_summary<IPL>(vv, vmin, jc0, A.tol, el, ei, eq, efn);
-        // stall bookkeeping (simplex.py:132-137), min-index switch (:123,138)
-        // and the objective check (:133): every block, from the same values
-        if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
-            nstd += 1;
-            const double z = -v0;
-            const double band = A.tol.stall * fmax(1.0, fabs(z0));
-            if (z - z0 > band) stop = 1;
-            if (fabs(z - z0) <= band) stuck += 1;
-            else stuck = 0;
-            if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
+        sel_summary<IPL>(vv, pv, vmin, jc0, tol, el, ei, eq, epc, efn);
+        const bool more = t + 1 < count;
+        const unsigned etag = gtag(seq, t, 1);
+        if (more) sel_put(grE, b, etag, esum_word(el, eq, ei, efn, epc), SEL_NGE, fast);
+        SEL_CLK(11);
+        // ---- while the summaries travel: the pivot-row values into LDS,
+        //      column 0 of the own rows (this pivot's multiplier is a), the
+        //      pivot row's register state, the stall bookkeeping, records
+        SelPoll<SEL_NGE> pe;
+        if (more) pe.issue(grE, G);
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                if (cok[k]) lP[kc[k] * CS + t] = pv[k];
+                l0v[k] = vn[k];
+            }
+            if (own) lcv = (li == R) ? p0 : fma(-a, p0, lcv);
+            if (R >= lr0 && R < lr1) {        // uniform: the leaving row is one of this block's
+                const bool mine = li == R;
+                m0 = mine ? (d16)0.0 : m0;
+                if (t >= 16) m1 = mine ? (d16)0.0 : m1;
+                if (NK > 2 && t >= 32) m2 = mine ? (d16)0.0 : m2;
+                if (NK > 3 && t >= 48) m3 = mine ? (d16)0.0 : m3;
+                if (mine) pstar = t;
+            }
+            if (lane == t) sRv = R;
+            // stall bookkeeping (simplex.py:132-137), min-index switch
+            // (:123,138) and the objective check (:133): every block, from
+            // the same values
+            if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
+                nstd += 1;
+                const double z = -v0;
+                const double band = tol.stall * fmax(1.0, fabs(z0));
+                if (z - z0 > band) stop = 1;
+                if (fabs(z - z0) <= band) stuck += 1;
+                else stuck = 0;
+                if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
+            }
+            if (b == G - 1 && lane < 7) {
+                long long *adr = &dRv[t];
+                long long val = R;
+                if (lane == 1) { adr = &dCv[t]; val = C; }
+                else if (lane == 2) { adr = &ctlv->r; val = rglob; }
+                else if (lane == 3) { adr = &ctlv->npiv; val = npiv + 1; }
+                else if (lane == 4) { adr = &ctlv->ndef[grp]; val = t + 1; }
+                else if (lane == 5) { adr = logv + 2 * min(npiv, logcapv - 1); val = rglob; }
+                else if (lane == 6) { adr = logv + 2 * min(npiv, logcapv - 1) + 1; val = C - 1; }
+                if (lane < 5 || npiv < logcapv) *gp(adr) = val;
+            }
+            if (b == 0 && lane == 0 && mode == MODE_SOLVE) {
+                *gp(&ctlv->nstd) = nstd;
+                *gp(&ctlv->stuck) = stuck;
+                *gp(&ctlv->rule) = rule;
+            }
+            ++npiv;
+            ++ndone;
+        if (!more) {
+            if (lane == 0) {                  // the next launch reads plain summaries
+                *gp(&erecv[b].l) = el;
+                *gp(&erecv[b].i) = ei;
+                *gp(&erecv[b].q) = eq;
+                *gp(&erecv[b].fneg) = efn;
+            }
+            break;
         }
-        stamp(Ar, b, t, 10);
+        // ---- the next pivot's entering column
+        SEL_CLK(12);
+        unsigned we[SEL_NGE];
+        if (!pe.finish(etag, we, &ctlv->bar_timeout, spinv)) {
+            status = LP_DEVICE_ERROR;
+            break;
+        }
+        SEL_CLK(13);
+        rule = __builtin_amdgcn_readfirstlane(rule);
+        stop = __builtin_amdgcn_readfirstlane(stop);
         {
-            unsigned wv = 0;
-            if (lane == 0) wv = lo32(el);
-            else if (lane == 1) wv = hi32(el);
-            else if (lane == 2) wv = lo32(eq);
-            else if (lane == 3) wv = hi32(eq);
-            else if (lane == 4) wv = idx32(ei);
-            else if (lane == 5) wv = idx32(efn);
-            drain_stores();
-            sel_put(grE, b, gtag(seq, t, 1), wv, SEL_NGE, fast);
+            const bool in = (unsigned)lane < G;
+            const double el2 = in ? mk_d(we[0], we[1]) : INFINITY;
+            const double eq2 = mk_d(we[2], we[3]);
+            const long long ef2 = in ? un_idx(we[5]) : NONE;
+            const bool capped = cap >= 0 && npiv >= cap;
+            long long Cn = NONE;
+            int owner = -1;                   // the block that answers (rescan / min-index)
+            double ethr = 0.0;
+            if (stop || capped) {
+                Cn = NONE;
+            } else if (rule == LP_RULE_MIN_INDEX) {
+                Cn = wave_min_ll(ef2);
+                if (Cn != NONE) owner = (int)((Cn - 1) / cpb);
+            } else {
+                const double g2 = wave_min(el2);
+                if (g2 < -tol.cost) {
+                    ethr = tie_band(g2, tol.cost_tie);
+                    const int bs = __builtin_ctzll(__ballot(in && el2 <= ethr));
+                    const double qs = rl_d(we[2], we[3], bs);
+                    if (qs <= ethr) {
+                        Cn = un_idx(rl32(we[4], bs));
+                        f0 = qs;
+                        pcw = rl_d(we[6], we[7], bs);
+                    } else {
+                        owner = bs;           // rare: the first column of its slice inside the band
+                    }
+                }
+            }
+            if (owner >= 0) {
+                // the owning block answers: the column, its row-0 value and
+                // P[t][column] from its registers (one more hand-off)
+                const unsigned atag = gtag(seq, t + 1, 6);
+                if (b == (unsigned)owner) {
+                    long long cc = Cn;
+                    int kf = 0, lf = 0;
+                    if (cc == NONE) {
+                        bool found = false;
+#pragma unroll
+                        for (int k = 0; k < IPL; ++k) {
+                            const u64 mk = __ballot(cok[k] && vn[k] <= ethr);
+                            if (!found && mk) {
+                                found = true;
+                                kf = k;
+                                lf = __builtin_ctzll(mk);
+                            }
+                        }
+                        cc = jc0 + 64 * kf + lf;
+                    } else {
+                        kf = (int)((cc - jc0) >> 6);
+                        lf = (int)((cc - jc0) & 63);
+                    }
+                    double fv = 0.0, pvv = 0.0;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k)
+                        if (k == kf) {
+                            fv = rl_d(lo32(vn[k]), hi32(vn[k]), lf);
+                            pvv = rl_d(lo32(pv[k]), hi32(pv[k]), lf);
+                        }
+                    unsigned wv = 0;
+                    if (lane == 0) wv = (unsigned)cc;
+                    else if (lane == 1) wv = lo32(fv);
+                    else if (lane == 2) wv = hi32(fv);
+                    else if (lane == 3) wv = lo32(pvv);
+                    else if (lane == 4) wv = hi32(pvv);
+                    sel_put(grS + 8, 0, atag, wv, SEL_NGS, fast);
+                }
+                unsigned y[SEL_NGS];
+                if (!sel_gather<SEL_NGS>(grS + 8, 1, atag, y, &ctlv->bar_timeout, spinv)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                Cn = (long long)rl32(y[0], 0);
+                f0 = rl_d(y[1], y[2], 0);
+                pcw = rl_d(y[3], y[4], 0);
+            }
+            (void)eq2;
+            C = Cn;
+            if (C == NONE) status = stop ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
-        bstamp(Ar, b, t, 1);
-        stamp(Ar, b, t, 11);
-        // ---- while the summaries travel: column 0 of the own rows (this
-        //      pivot's multiplier is a), the pivot row's register state, records
-        if (own) lcv = (li == R) ? p0 : fma(-a, p0, lcv);
-        if (R >= lr0 && R < lr1) {            // uniform: the leaving row is one of this block's
-            const bool mine = li == R;
-            m0 = mine ? (d16)0.0 : m0;
-            if (t >= 16) m1 = mine ? (d16)0.0 : m1;
-            if (NK > 2 && t >= 32) m2 = mine ? (d16)0.0 : m2;
-            if (NK > 3 && t >= 48) m3 = mine ? (d16)0.0 : m3;
-            if (mine) pstar = t;
-        }
-        if (lane == t) sRv = R;
-        if (b == G - 1 && lane < 7) {
-            long long *adr = &A.dR[t];
-            long long val = R;
-            if (lane == 1) { adr = &A.dC[t]; val = C; }
-            else if (lane == 2) { adr = &ctl->r; val = rglob; }
-            else if (lane == 3) { adr = &ctl->npiv; val = npiv + 1; }
-            else if (lane == 4) { adr = &ctl->ndef[grp]; val = t + 1; }
-            else if (lane == 5) { adr = A.log + 2 * min(npiv, A.logcap - 1); val = rglob; }
-            else if (lane == 6) { adr = A.log + 2 * min(npiv, A.logcap - 1) + 1; val = C - 1; }
-            if (lane < 5 || npiv < A.logcap) st_x(adr, val, fast);
-        }
-        if (b == 0 && lane == 0 && mode == MODE_SOLVE) {
-            st_x(&ctl->nstd, nstd, fast);
-            st_x(&ctl->stuck, stuck, fast);
-            st_x(&ctl->rule, rule, fast);
-        }
-        if (t == count - 1 && lane == 0) {    // the next launch reads plain summaries
-            st_x(&A.erec[b].l, el, fast);
-            st_x(&A.erec[b].i, ei, fast);
-            st_x(&A.erec[b].q, eq, fast);
-            st_x(&A.erec[b].fneg, efn, fast);
-        }
-        ++npiv;
-        ++ndone;
+        SEL_CLK(0);
     }
+#ifdef LPK_STAMPS
+    if (A.stamps && lane == 0) {
+        long long *o = A.stamps + BMAX * 16 + (long long)b * 32;
+        for (int k = 0; k < 16; ++k) o[k] = (long long)clk_[k];
+        o[16] = ndone;
+        o[17] = (long long)(__builtin_amdgcn_s_memrealtime() - clk_r0);   // 100 MHz ticks of the pivots
+        o[18] = (long long)(clk_t - 0);
+    }
+#endif
     // the sweep's copy of the launch's multipliers (MQ, 4-row quads), column 0
-    // of the own rows and row 0 / column 0's corner: read after the launch
+    // of the own rows, row 0 on the own columns and its corner: read after
+    // the launch
     {
         const int nds = __builtin_amdgcn_readfirstlane(ndone);
 #pragma unroll
         for (int s = 0; s < NB; ++s)
             if (s < nds && own) {
                 const d16 &mk = (s >> 4) == 0 ? m0 : (s >> 4) == 1 ? m1 : (s >> 4) == 2 ? m2 : m3;
-                *gp(&A.MQ[mq(li, s)]) = mk[s & 15];
+                *gp(&MQv[mq(li, s)]) = mk[s & 15];
             }
-        if (own) *gp(&A.col0[li]) = lcv;
+        if (own) *gp(&col0v[li]) = lcv;
+#pragma unroll
+        for (int k = 0; k < IPL; ++k)
+            if (cok[k]) *gp(&row0v[jk[k]]) = l0v[k];
         if (b == 0 && lane == 0) {
-            *gp(&A.row0[0]) = v0;
-            *gp(&A.col0[0]) = v0;
+            *gp(&row0v[0]) = v0;
+            *gp(&col0v[0]) = v0;
         }
+    }
+    if (XR && b == 0 && lane == 0) {
+        *gp(&ctl->xwait_ticks) += xwait;
+        *gp(&ctl->xwait_pivots) += ndone;
     }
     if (b == 0 && lane == 0) {
         // an increase at the launch's last pivot: nothing read the flag yet

@@ -87,6 +87,7 @@ _PROTOS = {
     "lp_peer_enable": (C.c_int, [_H, C.c_int]),
     "lp_set_host_allgather": (C.c_int, [_H, C.c_void_p, C.c_void_p]),
     "lp_exchange_path": (C.c_int, [_H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "lp_xwait": (C.c_int, [_H, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "lp_last_error": (C.c_char_p, [_H]),
 }
 
@@ -306,6 +307,13 @@ class Engine:
         p, f = C.c_int(), C.c_int()
         self.lib.lp_exchange_path(self.h, C.byref(p), C.byref(f))
         return p.value, f.value
+
+    def xwait(self):
+        """-> (cross-rank hop seconds, pivots) of the row-sharded persistent
+        selection, cumulative (lp_xwait: block 0, 100 MHz device clock)"""
+        t, n = C.c_int64(), C.c_int64()
+        self.lib.lp_xwait(self.h, C.byref(t), C.byref(n))
+        return t.value * 1e-8, n.value
 
     def set_block(self, pivots_per_sweep: int):
         """pivots deferred into one sweep of the tableau (1..64; 0 = auto)"""

@@ -192,7 +192,8 @@ class Simplex:
         try:
             res = tab._engine().find(rule, do_pivot)
         except _lib.DeviceError:
-            tab._device_failed()
+            if do_pivot:                   # only a pivoting call can have changed the tableau
+                tab._device_failed()
             raise
         if do_pivot and isinstance(res, tuple):
             tab._device_changed()
@@ -224,7 +225,8 @@ class Simplex:
         try:
             res = tab._engine().find_max_increase(do_pivot)
         except _lib.DeviceError:
-            tab._device_failed()
+            if do_pivot:
+                tab._device_failed()
             raise
         if do_pivot and isinstance(res, tuple):
             tab._device_changed()

@@ -66,6 +66,7 @@ class Tableau:
         self._eng: _lib.Engine | None = None
         self._host_ok = True     # host mirror is current
         self._dev_ok = False     # device tableau is current
+        self._lost = False       # a device failure took the only current copy
         self._tol: dict = {}
 
     # ------------------------------------------------------------------ sync
@@ -115,7 +116,7 @@ class Tableau:
             self._lost = True
 
     def _check_lost(self):
-        if getattr(self, '_lost', False):
+        if self._lost:
             raise _lib.DeviceError('tableau lost in an earlier device failure')
 
     def setTolerances(self, **kw):
@@ -160,6 +161,7 @@ class Tableau:
 
     def getZ(self) -> float:
         ''' objective value (-z) '''
+        self._check_lost()
         if not self._host_ok:
             return self._eng.objective()
         return float(-self._T[0, 0]) + 0.0
@@ -405,7 +407,8 @@ class Tableau:
         self._T = T
         self._cl = [str(data['cl'][j]) for j in range(n)]
         self._cm = [bool(data['cm'][j]) for j in range(n)]
-        self._host_ok, self._dev_ok = True, False
+        # a whole new tableau: whatever an earlier device failure lost is gone
+        self._host_ok, self._dev_ok, self._lost = True, False, False
 
     def saveJson(self) -> dict[str, Any]:
         ''' same keys and number strings as the reference (tableau.py:348-360);

@@ -383,6 +383,12 @@ for step in "$@"; do
             grep -H "^avg\|^pcomp" "$OUT"/stamps3_*.log ;;
         r3f)
             run r3f 300 python -u -m pytest tests/test_gpu_r2.py -k timeout -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        clk)
+            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
+            for B in ${CLK_BLOCKS:-48}; do
+                LPGPU_LIB=$L run clk_b$B 300 python scripts/sel_clocks.py mixed 4096 4096 $B
+                cat "$OUT/clk_b$B.log"
+            done ;;
         r3p)
             run r3p 600 python -u -m pytest tests/test_gpu_r3.py -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         *) echo "unknown step $step"; exit 2 ;;

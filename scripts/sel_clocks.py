@@ -1,0 +1,56 @@
+"""k_sel phase breakdown (diagnostic build, LPGPU_STAMPS=1): every block keeps
+per-phase shader-cycle sums in scalar registers for a whole launch and stores
+them once at its end (select.hip SEL_CLK).  Prints, per phase, the mean over
+blocks of cycles per pivot and the slowest block's, in cycles and in us at the
+clock measured over the launch (shader cycles / 100 MHz real-time ticks).
+
+    LPGPU_LIB=.../variants/stamps.so python scripts/sel_clocks.py [kind m ns block]
+"""
+import ctypes as C
+import os
+import sys
+
+os.environ["LPGPU_STAMPS"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
+from lpsol_amd import _lib, generators as gen  # noqa: E402
+
+kind, m, ns, blk = (sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])) \
+    if len(sys.argv) > 4 else ("mixed", 4096, 4096, 48)
+mm, n = gen.shape(kind, m, ns)
+e = _lib.Engine(mm, n)
+for a in range(0, mm + 1, 2048):
+    e.put_rows(a, gen.rows(kind, m, ns, 3, a, min(a + 2048, mm + 1)))
+e.set_block(blk)
+e.run(0, 4 * blk)
+e.run(0, blk)                      # the launch whose clocks are read
+geo = e.geometry()
+print("workload", kind, m, ns, "block", blk, "geometry", geo)
+assert geo["kernel"] == "k_sel", "not the one-XCD kernel"
+BMAX = 64
+buf = (C.c_longlong * (256 * BMAX * 4))()
+assert e.lib.lpdiag_bstamps(e.h, buf) == 0
+G = geo["blocks"]
+names = {1: "issue", 2: "colload", 3: "colchain", 4: "ratio", 5: "rpub", 6: "rgather", 7: "leave",
+         8: "rowload", 9: "rowchain", 10: "div", 11: "rowfin+epub", 12: "tail", 13: "egather", 0: "decide"}
+order = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 0]
+per = []
+clk = []
+for b in range(G):
+    o = buf[b * 32:b * 32 + 32]
+    nd = o[16]
+    if nd <= 1:
+        continue
+    # phase 0 and 12/13 run nd - 1 times (no next pivot after the last)
+    per.append({k: o[k] / (nd - 1 if k in (0, 12, 13) else nd) for k in order})
+    if o[17] > 0:
+        clk.append(sum(o[k] for k in order) / (o[17] * 10.0))   # cycles per ns -> GHz
+ghz = sorted(clk)[len(clk) // 2] if clk else 2.1
+print(f"blocks {len(per)}, shader clock ~{ghz:.2f} GHz (cycles / real time over the launch)")
+tot_mean = 0.0
+for k in order:
+    v = [p[k] for p in per]
+    mean = sum(v) / len(v)
+    tot_mean += mean
+    print(f"{names[k]:>12s}  mean {mean:7.0f} cyc {mean / ghz / 1000:5.2f} us   max {max(v):7.0f}   min {min(v):7.0f}")
+print(f"{'sum':>12s}  mean {tot_mean:7.0f} cyc {tot_mean / ghz / 1000:5.2f} us per pivot")

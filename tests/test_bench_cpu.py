@@ -89,3 +89,15 @@ def test_cpu_baseline_sample_runs():
     r = bench.cpu_baseline("cfg3", seconds_target=0.5)
     assert r["cores"] == 1 and r["kind"] == "port" and r["value"] > 0
     assert "pivot_dense" in r["sample"]
+
+
+def test_cpu_baseline_mid_run_sample():
+    """the cpu_baseline's later-pivot point: the first pivots (here the
+    reference's own cfg3 prefix, tests/golden/r3.json) replayed exactly on row
+    0, the pivot rows and a sample, then pivot #(k+1) timed on the sample"""
+    from conftest import load_golden
+    seq = [tuple(p) for p in load_golden("r3.json")["standard_k"][0]["seq"]]
+    r = bench.cpu_baseline("cfg3", seconds_target=0.5, seq=seq, k_mid=3)
+    assert r["kind"] == "port" and r["cores"] == 1 and r["value"] > 0
+    assert "seconds_per_pivot_at_1" in r and "seconds_per_pivot_at_4" in r
+    assert r["seconds_per_pivot"] == r["seconds_per_pivot_at_4"]

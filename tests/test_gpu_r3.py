@@ -146,3 +146,46 @@ def test_sel_shapes_bit_exact(m, ns, kind, block):
     assert np.array_equal(e.download(), o.T)
     assert e.geometry()["kernel"] == "k_sel"
     e.close()
+
+
+# ------------------------------------------- the two-level exchange's rare paths
+TALL = ("tall", 16500, 40, 36)
+
+
+def test_two_level_timeout_recovery(monkeypatch):
+    """fault injection on a shape that takes k_group's two-level
+    exchange (16500 rows, blocks spread over the XCDs): block 1 withholds a
+    ratio summary, its XCD group's combine times out, the host redoes the
+    group on the per-pivot kernels -- sequence and tableau as without it"""
+    monkeypatch.setenv("LPGPU_FAULT", "1:3")
+    monkeypatch.setenv("LPGPU_SPIN_MAX", "20000")
+    monkeypatch.delenv("LPGPU_STRICT", raising=False)
+    T = gen.tableau(*TALL)
+    e = _engine(T, 64)
+    st, done = e.run(_lib.RULE_STANDARD, 40)
+    o = F64Tableau(T)
+    ost, olog = o.run(0, 40)
+    assert e.log().tolist() == olog.tolist()
+    assert np.array_equal(e.download(), o.T)
+    assert e.exchange_path() == (_lib.PATH_KERNELS, 1)
+    e.close()
+
+
+def test_two_level_objective_increased():
+    """Simplex.solve's 'objective value increased' stop
+    (simplex.py:133) on the two-level exchange: a negative b makes the first
+    pivot raise the objective; status, pivots and tableau as the f64 oracle's"""
+    T = gen.tableau(*TALL)
+    o0 = F64Tableau(T)
+    r, c = o0.find(0)
+    T[1 + r, 0] = -1.0 / 64           # the row the ratio test picks first
+    e = _engine(T, 64)
+    st, npiv, nstd = e.solve()
+    o = F64Tableau(T)
+    ost, olog, onstd = o.solve()
+    assert st == ost == _lib.OBJ_INCREASED
+    assert e.log().tolist() == olog.tolist()
+    assert np.array_equal(e.download(), o.T)
+    geo = e.geometry()
+    assert geo["kernel"] == "k_group" and geo["two_level_engaged"], geo
+    e.close()

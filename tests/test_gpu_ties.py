@@ -87,4 +87,6 @@ def test_spread_selection_two_level_exchange(rule, tie):
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), o.T)
     assert e.exchange_path() == (_lib.PATH_PERSISTENT, 0)
+    geo = e.geometry()                 # the two-level exchange really engaged
+    assert geo["kernel"] == "k_group" and geo["two_level_engaged"], geo
     e.close()
