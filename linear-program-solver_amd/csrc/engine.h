@@ -87,7 +87,8 @@ struct Ctl {
     unsigned bar[2];     // unused (kept zero)
     unsigned bar_timeout;// set if a k_group exchange gave up (never expected)
     unsigned sel_flags;  // the last persistent selection launch (block 0): 1 every block on one XCD,
-                         // 2 the two-level exchange engaged (k_group), 4 the one-XCD kernel k_sel ran
+                         // 2 the two-level exchange engaged (k_group), 4 the one-XCD kernel k_sel ran,
+                         // 8 k_sel found its blocks on several XCDs (group abandoned, redone by the host)
     // k_group: the loop state at the start of the launch (every block writes
     // the same values before any pivot of the group: a timeout is only seen
     // by a block that ran, so the snapshot is always the failing launch's,

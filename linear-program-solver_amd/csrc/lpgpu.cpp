@@ -1140,7 +1140,9 @@ static int recover_timeout(const Members &M, const std::vector<Args> &A, int mod
         h->hctl->npiv = c.npiv;
         h->hctl->status = LP_PIVOTED;
         h->hctl->bar_timeout = 0;
-        h->err = "a persistent selection group timed out; it was redone on the per-pivot kernels";
+        h->err = (c.sel_flags & 8u) ? "the one-XCD selection's blocks were not on one XCD; the group was redone on "
+                                      "the per-pivot kernels"
+                                    : "a persistent selection group timed out; it was redone on the per-pivot kernels";
     }
     return LP_PIVOTED;
 }
@@ -1685,7 +1687,8 @@ extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
 // own columns per lane, own rows per lane, summaries per lane, one-XCD grid,
 // k_group's two-level variant, k_sel's pivot capacity (0: k_group),
 // Ctl::sel_flags of the last launch (1 one XCD, 2 two-level exchange engaged,
-// 4 k_sel); all 0 when the per-pivot kernels run
+// 4 k_sel, 8 k_sel's blocks were not on one XCD); all 0 when the per-pivot
+// kernels run
 extern "C" int lpdiag_geometry(lp_handle *h, long long *out)
 {
     const Members M = members_of(h);

@@ -64,15 +64,23 @@ namespace {
         const int z_ = __builtin_amdgcn_readfirstlane((int)__double_as_longlong(x)); \
         asm volatile("s_nop 0" ::"s"(z_));                                        \
     } while (0)
+// per pivot t < 48 and block: 100 MHz real-time stamps of phase points
+// (scripts/sel_clocks.py --events): 0 pivot start, 1 column arrived, 2 ratio
+// summary published, 3 every ratio summary seen, 4 row-0 summary published,
+// 5 every row-0 summary seen
+#define SEL_EV(k)                                                                                   \
+    do {                                                                                            \
+        if (A.stamps && lane == 0 && t < 48)                                                        \
+            *gp(A.stamps + BMAX * 16 + 4096 + ((long long)t * 64 + b) * 8 + (k)) =                  \
+                (long long)__builtin_amdgcn_s_memrealtime();                                        \
+    } while (0)
 #else
 #define SEL_CLK_DECL
 #define SEL_CLK(k) do {} while (0)
 #define SEL_DONE(x) do {} while (0)
+#define SEL_EV(k) do {} while (0)
 #endif
 
-constexpr int SEL_NGR = 7;   // ratio summary: l (2), i, a (2), b (2)
-constexpr int SEL_NGE = 8;   // row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
-constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
 typedef double d16 __attribute__((ext_vector_type(16)));
 
 // ---- deferred-pivot chains --------------------------------------------------
@@ -121,41 +129,47 @@ struct RowPair;
 #define SEL_RF(XI, MI, PI, L) "v_fmac_f64_dpp %" #XI ", -%" #MI ", %" #PI " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
 template <>
 struct RowPair<1> {
-    template <int L0, int L1>
+    template <int L0, int L1, bool NOP>
     static __device__ __forceinline__ void run(double (&x)[1], double mr, const double2 (&p)[1]);
 };
 template <>
 struct RowPair<2> {
-    template <int L0, int L1>
+    template <int L0, int L1, bool NOP>
     static __device__ __forceinline__ void run(double (&x)[2], double mr, const double2 (&p)[2]);
 };
 template <>
 struct RowPair<4> {
-    template <int L0, int L1>
+    template <int L0, int L1, bool NOP>
     static __device__ __forceinline__ void run(double (&x)[4], double mr, const double2 (&p)[4]);
 };
-#define SEL_PAIR_DEF(L0, L1)                                                                              \
+// (NOP: the chain's first pair waits out the DPP hazard of the broadcast
+// operands' VALU writes; later pairs read the same, unchanged registers)
+#define SEL_PAIR_DEF1(L0, L1, NOP, PRE)                                                                    \
     template <>                                                                                           \
-    __device__ __forceinline__ void RowPair<1>::run<L0, L1>(double (&x)[1], double mr, const double2 (&p)[1]) \
+    __device__ __forceinline__ void RowPair<1>::run<L0, L1, NOP>(double (&x)[1], double mr,                \
+                                                                 const double2 (&p)[1])                   \
     {                                                                                                     \
-        asm("s_nop 4\n" SEL_RF(0, 1, 2, L0) SEL_RF(0, 1, 3, L1) : "+v"(x[0]) : "v"(mr), "v"(p[0].x), "v"(p[0].y)); \
+        asm(PRE SEL_RF(0, 1, 2, L0) SEL_RF(0, 1, 3, L1) : "+v"(x[0]) : "v"(mr), "v"(p[0].x), "v"(p[0].y));  \
     }                                                                                                     \
     template <>                                                                                           \
-    __device__ __forceinline__ void RowPair<2>::run<L0, L1>(double (&x)[2], double mr, const double2 (&p)[2]) \
+    __device__ __forceinline__ void RowPair<2>::run<L0, L1, NOP>(double (&x)[2], double mr,                \
+                                                                 const double2 (&p)[2])                   \
     {                                                                                                     \
-        asm("s_nop 4\n" SEL_RF(0, 2, 3, L0) SEL_RF(1, 2, 5, L0) SEL_RF(0, 2, 4, L1) SEL_RF(1, 2, 6, L1)    \
+        asm(PRE SEL_RF(0, 2, 3, L0) SEL_RF(1, 2, 5, L0) SEL_RF(0, 2, 4, L1) SEL_RF(1, 2, 6, L1)            \
             : "+v"(x[0]), "+v"(x[1])                                                                      \
             : "v"(mr), "v"(p[0].x), "v"(p[0].y), "v"(p[1].x), "v"(p[1].y));                                \
     }                                                                                                     \
     template <>                                                                                           \
-    __device__ __forceinline__ void RowPair<4>::run<L0, L1>(double (&x)[4], double mr, const double2 (&p)[4]) \
+    __device__ __forceinline__ void RowPair<4>::run<L0, L1, NOP>(double (&x)[4], double mr,                \
+                                                                 const double2 (&p)[4])                   \
     {                                                                                                     \
-        asm("s_nop 4\n" SEL_RF(0, 4, 5, L0) SEL_RF(1, 4, 7, L0) SEL_RF(2, 4, 9, L0) SEL_RF(3, 4, 11, L0)   \
+        asm(PRE SEL_RF(0, 4, 5, L0) SEL_RF(1, 4, 7, L0) SEL_RF(2, 4, 9, L0) SEL_RF(3, 4, 11, L0)           \
                 SEL_RF(0, 4, 6, L1) SEL_RF(1, 4, 8, L1) SEL_RF(2, 4, 10, L1) SEL_RF(3, 4, 12, L1)           \
             : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3])                                              \
             : "v"(mr), "v"(p[0].x), "v"(p[0].y), "v"(p[1].x), "v"(p[1].y), "v"(p[2].x), "v"(p[2].y),      \
               "v"(p[3].x), "v"(p[3].y));                                                                  \
     }
+#define SEL_PAIR_DEF(L0, L1) SEL_PAIR_DEF1(L0, L1, true, "s_nop 4\n") SEL_PAIR_DEF1(L0, L1, false, "")
 SEL_PAIR_DEF(0, 1)
 SEL_PAIR_DEF(2, 3)
 SEL_PAIR_DEF(4, 5)
@@ -165,6 +179,7 @@ SEL_PAIR_DEF(10, 11)
 SEL_PAIR_DEF(12, 13)
 SEL_PAIR_DEF(14, 15)
 #undef SEL_PAIR_DEF
+#undef SEL_PAIR_DEF1
 #undef SEL_RF
 #undef SEL_F
 
@@ -184,12 +199,16 @@ template <int IPL, int NB, int H>
 __device__ __forceinline__ void row_steps(double (&x)[IPL], const double (&mr)[NB / 16], const double *lP,
                                           const int (&kc)[IPL], int t, double2 (&ring)[4][IPL])
 {
-    if (2 * H >= t) return;
+    // t checked every second pair: the pivots of a pair past t have m = 0 and
+    // P = 0 (LDS zeroed at launch start), exact no-ops
+    if constexpr ((H & 1) == 0) {
+        if (2 * H >= t) return;
+    }
     lds_pair<IPL, NB>(ring[(H + 3) & 3], lP, kc, H + 3);
     // keep the read-ahead: without the barrier the scheduler sinks each read
     // to its FMAs and every pair waits out a full LDS latency
     __builtin_amdgcn_sched_barrier(0);
-    RowPair<IPL>::template run<2 * (H & 7), 2 * (H & 7) + 1>(x, mr[H >> 3], ring[H & 3]);
+    RowPair<IPL>::template run<2 * (H & 7), 2 * (H & 7) + 1, H == 0>(x, mr[H >> 3], ring[H & 3]);
     if constexpr (H + 1 < NB / 2) row_steps<IPL, NB, H + 1>(x, mr, lP, kc, t, ring);
 }
 template <int IPL, int NB>
@@ -211,10 +230,13 @@ __device__ __forceinline__ void row_chain(double (&x)[IPL], const double (&mr)[N
 // immediate offset (the per-granule addresses of the general layout, kept
 // live across the pivot loop, cost k_sel about 70 VGPRs).
 constexpr int SEL_SLOT = 64;
+#ifndef SEL_SLEEP
+#define SEL_SLEEP 1            // s_sleep between the polls of an exchange (64 clocks per unit)
+#endif
 // a loop-invariant operand moved into a VGPR (the asm makes it look
-// divergent, so it stays there): k_sel keeps its kernel arguments, per-block
-// constants and tolerances in VGPRs -- in SGPRs the compiler ran out (106)
-// and spilled about 70 of them into VGPR lanes, a v_readlane per use
+// divergent, so it stays there): k_sel keeps most of its kernel arguments,
+// per-block constants and tolerances in VGPRs -- in SGPRs the compiler ran
+// out (106) and spilled about 70 of them into VGPR lanes, a v_readlane per use
 template <typename T>
 __device__ __forceinline__ T vgpr(T x)
 {
@@ -222,10 +244,74 @@ __device__ __forceinline__ T vgpr(T x)
     return x;
 }
 
-// the words of a summary: lane g (< n) stores word g of block b
-__device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, unsigned w, int n, bool fast)
+// p + byte offset: with p wave-uniform and a 32-bit per-lane offset the
+// access is one global instruction with a scalar base (no per-lane 64-bit
+// address arithmetic)
+template <typename T>
+__device__ __forceinline__ T *at(T *p, unsigned off)
 {
-    if ((int)threadIdx.x < n) st_x(&region[threadIdx.x * SEL_SLOT + b], ((u64)tag << 32) | w, fast);
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(p) + off);
+}
+template <typename T>
+__device__ __forceinline__ const T *at(const T *p, unsigned off)
+{
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(p) + off);
+}
+
+// hand-off store: FAST (every block on one XCD, checked at launch start) is a
+// plain store that stays in the XCD's L2, else write-through (device.h st_x)
+template <bool FAST, typename T>
+__device__ __forceinline__ void stx(T *p, T v)
+{
+    if constexpr (FAST) __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else st_sc1(p, v);
+}
+
+// minimum of two doubles as v_min_f64 computes it, without the NaN
+// canonicalisation fmin() adds (no operand here is a NaN); the s_nop covers
+// the two wait states a DPP read of the result needs after this VALU write
+__device__ __forceinline__ double vmin(double a, double b)
+{
+    double r;
+    asm("v_min_f64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ double dppd(double v)
+{
+    const u64 x = (u64)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)x, CTRL, RM, 0xf, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(x >> 32), CTRL, RM, 0xf, false);
+    return mk_d(lo, hi);
+}
+// wave minimum (all 64 lanes active), wave-uniform: two quad permutes and two
+// row rotates reduce each row of 16, two row broadcasts fold the rows into
+// lane 63 (the other lanes end with partial or undefined values)
+__device__ __forceinline__ double wmin(double v)
+{
+    v = vmin(v, dppd<0xB1, 0xf>(v));
+    v = vmin(v, dppd<0x4E, 0xf>(v));
+    v = vmin(v, dppd<0x124, 0xf>(v));
+    v = vmin(v, dppd<0x128, 0xf>(v));
+    v = vmin(v, dppd<0x142, 0xa>(v));
+    v = vmin(v, dppd<0x143, 0xc>(v));
+    return rl_d(lo32(v), hi32(v), 63);
+}
+// lane l's word of a summary assembled from wave-uniform values: v_writelane
+// per word (a select chain on the lane index compiled to a branch per word)
+template <int L>
+__device__ __forceinline__ unsigned wl_(unsigned w, unsigned v)
+{
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(__builtin_amdgcn_readfirstlane(v)), "n"(L));
+    return w;
+}
+#define wl(W, V, L) wl_<L>((W), (V))
+
+// the words of a summary: lane g (< n) stores word g of block b
+template <bool FAST>
+__device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, unsigned w, int n)
+{
+    if ((int)threadIdx.x < n) stx<FAST>(&region[threadIdx.x * SEL_SLOT + b], ((u64)tag << 32) | w);
 }
 // every block's summary (lane l: block min(l, G - 1)); polls until every
 // granule carries `tag`, bounded by spin_max polls (the host then redoes the
@@ -248,7 +334,7 @@ __device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (
             st_sc1(timeout_flag, 1u);
             return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(SEL_SLEEP);
     }
 }
 
@@ -258,11 +344,11 @@ __device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (
 // the tie band of el (ei, its value eq, and P[t][ei] = epc from pv), first
 // column with c_j < -tol.cost (efn)
 template <int IPL>
-__device__ __forceinline__ void sel_summary(const double (&vv)[IPL], const double (&pv)[IPL], double vmin,
+__device__ __forceinline__ void sel_summary(const double (&vv)[IPL], const double (&pv)[IPL], double vmin_,
                                             long long jc0, const lp_tol &tol, double &el, long long &ei,
                                             double &eq, double &epc, long long &efn)
 {
-    el = wave_min(vmin);
+    el = wmin(vmin_);
     efn = NONE;
     ei = NONE;
     eq = 0.0;
@@ -281,12 +367,18 @@ __device__ __forceinline__ void sel_summary(const double (&vv)[IPL], const doubl
         }
     }
 }
-// this lane's word of a row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
-__device__ __forceinline__ unsigned esum_word(double el, double eq, long long ei, long long efn, double epc)
+// the words of a row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
+__device__ __forceinline__ unsigned esum_words(double el, double eq, long long ei, long long efn, double epc)
 {
-    const int lane = threadIdx.x;
-    return lane == 0 ? lo32(el) : lane == 1 ? hi32(el) : lane == 2 ? lo32(eq) : lane == 3 ? hi32(eq)
-         : lane == 4 ? idx32(ei) : lane == 5 ? idx32(efn) : lane == 6 ? lo32(epc) : hi32(epc);
+    unsigned w = idx32(ei);
+    w = wl(w, lo32(el), 0);
+    w = wl(w, hi32(el), 1);
+    w = wl(w, lo32(eq), 2);
+    w = wl(w, hi32(eq), 3);
+    w = wl(w, idx32(efn), 5);
+    w = wl(w, lo32(epc), 6);
+    w = wl(w, hi32(epc), 7);
+    return w;
 }
 // sel_gather split in two: issue() sends the first polls, finish() checks them
 // (and polls on); work placed between the two runs while the polls are in
@@ -318,60 +410,42 @@ struct SelPoll {
                 st_sc1(timeout_flag, 1u);
                 return false;
             }
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(SEL_SLEEP);
 #pragma unroll
             for (int g = 0; g < NG; ++g) v[g] = ld_sc1(p + g * SEL_SLOT);
         }
     }
 };
 
-}  // namespace
+constexpr int SEL_NGR = 9;   // ratio summary: l (2), i, a (2), b (2), q of the candidate (2)
+constexpr int SEL_NGE = 8;   // row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
+constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
+constexpr int SEL_NGX = 7;   // XR rank summary: l (2), global row, a (2), b (2)
 
-// NB: most pivots of a launch (register multipliers); IPL: own columns per
-// lane (cpb <= 64 IPL); XR: one rank of a row-sharded job (leaving row and
-// pivot row exchanged between ranks through the peers' exchange buffers, as
-// in k_group).  first: as k_group's (call start: reset / eager / enter).
-template <int IPL, int NB, bool XR>
-__global__ void __launch_bounds__(GROUP_THREADS)
-k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int first, int fmode, int frule,
-      long long fcap)
+// The pivot loop of k_sel.  NB: most pivots of a launch (register
+// multipliers); IPL: own columns per lane (cpb <= 64 IPL); XR: one rank of a
+// row-sharded job (leaving row and pivot row exchanged between ranks through
+// the peers' exchange buffers, as in k_group); FAST: every block on one XCD.
+// first: as k_group's (call start: reset / eager / enter).
+template <int IPL, int NB, bool XR, bool FAST>
+__device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const unsigned G, int grp, int count,
+                                         int from_erec, unsigned seq, int first, int fmode, long long fcap,
+                                         double *lP, long long npiv, long long nstd, long long stuck, int rule)
 {
-    static_assert(NB % 16 == 0 && NB <= BMAX, "k_sel: pivots per launch");
-    // the grid is 8 x G and only blocks 0, 8, 16, ... work: they share one XCD
-    // under the round-robin dealing of workgroups (speed only: checked below)
-    if (blockIdx.x & 7u) return;
     constexpr int CS = NB + 2;             // LDS stride of a column's pivot values (16-B reads, no conflicts)
     constexpr int NK = NB / 16;            // broadcast registers
-    extern __shared__ __attribute__((aligned(16))) double lP[];   // [cpb][CS]: P[s][own column]
-    const unsigned b = blockIdx.x >> 3, G = (unsigned)gper;
     const int lane = threadIdx.x;
     Ctl *ctl = A.ctl;
     const bool reset = (first & 1) != 0, eager = (first & 2) != 0, enter = (first & 4) != 0;
-    if (b == 0 && lane == 0) *gp(&ctl->ndef[grp]) = 0;
-    if (!reset && (ld_sc1(&ctl->status) != LP_PIVOTED || ld_sc1(&ctl->bar_timeout) != 0u)) return;
     const long long cap = reset ? fcap : *gp(&ctl->cap);
     const int mode = reset ? fmode : *gp(&ctl->mode);
-    long long npiv = reset ? 0 : ld_sc1(&ctl->npiv);
-    int rule = reset ? frule : ld_sc1(&ctl->rule);
-    long long nstd = 0, stuck = 0;
-    if (!reset) {
-        nstd = ld_sc1(&ctl->nstd);
-        stuck = ld_sc1(&ctl->stuck);
-    }
-    rule = __builtin_amdgcn_readfirstlane(rule);
-    if (lane == 0) {
-        // the loop state before this group: what a timed-out group is redone from
-        st_sc1(&ctl->g_npiv, npiv);
-        st_sc1(&ctl->g_nstd, nstd);
-        st_sc1(&ctl->g_stuck, stuck);
-        st_sc1(&ctl->g_rule, rule);
-        st_sc1(&ctl->g_seq, seq);
-    }
-    // loop-invariant operands in VGPRs (vgpr())
+    // the tableau, pivot rows and multipliers stay scalar bases (one global
+    // instruction per access with a per-lane 32-bit offset); the other
+    // loop-invariant operands live in VGPRs (vgpr())
+    double *const Tb = A.T;
+    double *const Pb = A.P;
+    double *const Mb = A.M;
     const long long ld = vgpr(A.ld);
-    double *const Tv = vgpr(A.T);
-    double *const Pv = vgpr(A.P);
-    double *const Mv = vgpr(A.M);
     double *const MQv = vgpr(A.MQ);
     double *const row0v = vgpr(A.row0);
     double *const col0v = vgpr(A.col0);
@@ -395,21 +469,37 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     int jk[IPL];
     bool cok[IPL];
     int kc[IPL];
+    unsigned xoff[IPL];                    // byte offsets: own column in a row (clamped to the row)
 #pragma unroll
     for (int k = 0; k < IPL; ++k) {
         jk[k] = (int)jc0 + lane + 64 * k;
         cok[k] = jk[k] < jc1;
         kc[k] = (int)min((long long)lane + 64 * k, cpb - 1);
+        xoff[k] = vgpr((unsigned)min((long long)jk[k], nv) * 8u);
     }
+    // byte offsets of the broadcast operands: P[16 k + lane % 16][.] and
+    // M[16 k + lane % 16][.] (every row of P and M exists: NB <= BMAX)
+    unsigned pkoff[NK], mroff[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+        const unsigned s = 16u * k + (lane & 15);
+        pkoff[k] = vgpr(s * (unsigned)ld * 8u);
+        mroff[k] = vgpr(s * (unsigned)rowsv * 8u);
+    }
+    const unsigned moff = vgpr((unsigned)li * 8u);
+    // the row the lane's column element comes from: its tableau row, or the
+    // pivot row P[s*] once the lane's row was pivot row s* of this launch
+    const double *arow = vgpr(Tb + (own ? li : 0) * ld);
     // current row 0 on own columns, row0[0], column 0 of the own row: the
     // eager copies, or (first launch after an upload) the stored tableau's
     double l0v[IPL];
 #pragma unroll
-    for (int k = 0; k < IPL; ++k) l0v[k] = cok[k] ? (eager ? *gp(Tv + jk[k]) : *gp(row0v + jk[k])) : 0.0;
-    double v0 = eager ? *gp(Tv) : *gp(row0v);
-    double lcv = own ? (eager ? *gp(Tv + li * ld) : *gp(col0v + li)) : 0.0;
+    for (int k = 0; k < IPL; ++k) l0v[k] = cok[k] ? (eager ? *gp(Tb + jk[k]) : *gp(row0v + jk[k])) : 0.0;
+    double v0 = eager ? *gp(Tb) : *gp(row0v);
+    double lcv = own ? (eager ? *gp(Tb + li * ld) : *gp(col0v + li)) : 0.0;
     if (eager) {
-        // the other blocks read row0[C] (a pivot's row-0 multiplier)
+        // the other blocks read row0[C] (a pivot's row-0 multiplier); the
+        // entering-column exchange below drains these first
 #pragma unroll
         for (int k = 0; k < IPL; ++k)
             if (cok[k]) st_sc1(&row0v[jk[k]], l0v[k]);
@@ -420,51 +510,33 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     // summary regions: ratio, row 0, XCD check, rescan answers
     u64 *const grR = vgpr(A.gran);
     u64 *const grE = vgpr(A.gran + GROUP_MAXBLOCKS * GSLOT);
-    u64 *const grX = vgpr(A.gran + 2 * GROUP_MAXBLOCKS * GSLOT);
     u64 *const grS = vgpr(A.gran + 3 * GROUP_MAXBLOCKS * GSLOT);
     ERec *const erecv = vgpr(A.erec);
     long long *const logv = vgpr(A.log);
     long long *const dRv = vgpr(A.dR);
     long long *const dCv = vgpr(A.dC);
     const long long logcapv = vgpr(A.logcap);
-    const unsigned spinv = vgpr(A.spin_max);
+    const unsigned spin = A.spin_max;
     Ctl *const ctlv = vgpr(ctl);            // the loop's hand-off flags and records
     u64 *const xbufv = vgpr(A.xbuf);        // XR: this rank's exchange buffer, the peers'
     unsigned long long *const *const peerv = vgpr(A.peer);
     const long long rbv = vgpr(A.rb);
-    bool fast = false;
-    {
-        // every block publishes its XCD; plain (L2-resident) hand-off stores
-        // only if all match
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-        drain_stores();
-        if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | xcc);
-        unsigned wx[1];
-        if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctlv->bar_timeout, spinv)) {
-            if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
-            return;
-        }
-        const bool same = !((unsigned)lane < G) || wx[0] == xcc;
-        fast = __builtin_amdgcn_readfirstlane(__all(same) ? 1 : 0) != 0;
-    }
-    if (b == 0 && lane == 0) *gp(&ctl->sel_flags) = (fast ? 1u : 0u) | 4u;   // diagnostics
     double z0 = 0.0;
     if (reset) {
         z0 = -v0;                              // obj_val at the start (simplex.py:118)
         if (b == 0 && lane == 0) {
-            st_x(&ctl->status, (int)LP_PIVOTED, fast);
-            st_x(&ctl->mode, mode, fast);
-            st_x(&ctl->rule, rule, fast);
-            st_x(&ctl->chain, 1, fast);
-            st_x(&ctl->cap, cap, fast);
-            st_x(&ctl->r, -1LL, fast);
-            st_x(&ctl->c, -1LL, fast);
-            st_x(&ctl->npiv, 0LL, fast);
-            st_x(&ctl->nstd, 0LL, fast);
-            st_x(&ctl->stuck, 0LL, fast);
-            st_x(&ctl->z0, z0, fast);
-            st_x(&ctl->ndef[grp ^ 1], 0LL, fast);
+            stx<FAST>(&ctl->status, (int)LP_PIVOTED);
+            stx<FAST>(&ctl->mode, mode);
+            stx<FAST>(&ctl->rule, rule);
+            stx<FAST>(&ctl->chain, 1);
+            stx<FAST>(&ctl->cap, cap);
+            stx<FAST>(&ctl->r, -1LL);
+            stx<FAST>(&ctl->c, -1LL);
+            stx<FAST>(&ctl->npiv, 0LL);
+            stx<FAST>(&ctl->nstd, 0LL);
+            stx<FAST>(&ctl->stuck, 0LL);
+            stx<FAST>(&ctl->z0, z0);
+            stx<FAST>(&ctl->ndef[grp ^ 1], 0LL);
             st_sc1(&ctl->bar_timeout, 0u);
         }
     } else {
@@ -502,21 +574,21 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     ef = ld_sc1(&erecv[lane].fneg);
                 }
             } else {
-                double vv[IPL], vmin = INFINITY, pz[IPL];
+                double vv[IPL], vmn = INFINITY, pz[IPL];
 #pragma unroll
                 for (int k = 0; k < IPL; ++k) {
                     vv[k] = cok[k] ? l0v[k] : INFINITY;
-                    vmin = fmin(vmin, vv[k]);
+                    vmn = fmin(vmn, vv[k]);
                     pz[k] = 0.0;
                 }
                 double sel_, seq_, spc_;
                 long long sei_, sfn_;
-                sel_summary<IPL>(vv, pz, vmin, jc0, tol, sel_, sei_, seq_, spc_, sfn_);
+                sel_summary<IPL>(vv, pz, vmn, jc0, tol, sel_, sei_, seq_, spc_, sfn_);
                 const unsigned etag = gtag(seq, 0, 0);
                 drain_stores();
-                sel_put(grE, b, etag, esum_word(sel_, seq_, sei_, sfn_, spc_), SEL_NGE, fast);
+                sel_put<FAST>(grE, b, etag, esum_words(sel_, seq_, sei_, sfn_, spc_), SEL_NGE);
                 unsigned w[SEL_NGE];
-                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctlv->bar_timeout, spinv)) status = LP_DEVICE_ERROR;
+                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctlv->bar_timeout, spin)) status = LP_DEVICE_ERROR;
                 if (in) {
                     el = mk_d(w[0], w[1]);
                     eq = mk_d(w[2], w[3]);
@@ -529,7 +601,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             } else if (rule == LP_RULE_MIN_INDEX) {
                 C = wave_min_ll(ef);
             } else {
-                const double g = wave_min(el);
+                const double g = wmin(el);
                 if (g < -tol.cost) {
                     const double ethr = tie_band(g, tol.cost_tie);
                     double l1[1] = {el}, q1[1] = {eq};
@@ -556,19 +628,23 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             clk_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
         }
+        SEL_EV(0);
         // ---- one round trip: the own rows' elements of column C (a pivot row
         //      of this launch: P[pstar][C]) and P[s][C] of the earlier pivots
         //      for the broadcasts; P[t - 1][C] came with the summaries
         // (every load unconditional and the selects after the last one: a
         // select right after its load made the compiler wait for each load
         // in turn -- four round trips instead of one)
-        const double *ap = pstar >= 0 ? Pv + (long long)pstar * ld : Tv + (own ? li : 0) * ld;
-        double a = ld_sc1(ap + C);
+        const double *const cP = Pb + C;      // wave-uniform
+        double a = ld_sc1(arow + C);
         double pk[NK];
+        // rows past t - 2 read row t - 2 instead (discarded below): a row of
+        // this launch, in L2 -- a stale row of an earlier launch is an HBM miss
+        const unsigned pkc = (unsigned)max(t - 2, 0) * (unsigned)ld * 8u;
 #pragma unroll
-        for (int k = 0; k < NK; ++k)
-            pk[k] = ld_sc1(&Pv[(long long)max(min(16 * k + (lane & 15), t - 2), 0) * ld + C]);
-        a = own ? (pstar >= 0 && pstar == t - 1 ? pcw : a) : 0.0;
+        for (int k = 0; k < NK; ++k) pk[k] = ld_sc1(at(cP, 16 * k + (lane & 15) <= t - 2 ? pkoff[k] : pkc));
+        const bool apcw = pstar >= 0 && pstar == t - 1;
+        a = own ? (apcw ? pcw : a) : 0.0;
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
             const int sk = 16 * k + (lane & 15);
@@ -577,22 +653,25 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         SEL_CLK(1);
         if (STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: the column has arrived
         SEL_CLK(2);
+        SEL_EV(1);
         col_chain<NK>(a, pk, m0, m1, m2, m3, t);
         SEL_DONE(a);
         SEL_CLK(3);
-        // ---- ratio test over the own rows
+        // ---- ratio test over the own rows; the block's candidate: the first
+        //      row inside the band of the block minimum
         bool okq;
         const double q = row_ratio(a, lcv, tol, okq);
         okq = okq && own;
-        const double lb = wave_min(okq ? q : INFINITY);
+        const double lb = wmin(okq ? q : INFINITY);
         long long ib = NONE;
-        double ab = 0.0, bb = 0.0;
+        double ab = 0.0, bb = 0.0, qb = 0.0;
         if (lb < INFINITY) {
             const u64 mask = __ballot(okq && q <= tie_band(lb, tol.ratio_tie));
             const int f = __builtin_ctzll(mask);
             ib = lr0 + f;
             ab = rl_d(lo32(a), hi32(a), f);
             bb = rl_d(lo32(lcv), hi32(lcv), f);
+            qb = rl_d(lo32(q), hi32(q), f);
         }
         SEL_DONE(lb);
         SEL_CLK(4);
@@ -602,42 +681,46 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         drain_stores();
         if (!(A.fault == t + 1 && b == min(1u, G - 1))) {   // fault injection (tests): block 1 (0) never publishes
             unsigned wv = idx32(ib);
-            if (lane == 0) wv = lo32(lb);
-            else if (lane == 1) wv = hi32(lb);
-            else if (lane == 3) wv = lo32(ab);
-            else if (lane == 4) wv = hi32(ab);
-            else if (lane == 5) wv = lo32(bb);
-            else if (lane == 6) wv = hi32(bb);
-            sel_put(grR, b, gtag(seq, t, 0), wv, SEL_NGR, fast);
+            wv = wl(wv, lo32(lb), 0);
+            wv = wl(wv, hi32(lb), 1);
+            wv = wl(wv, lo32(ab), 3);
+            wv = wl(wv, hi32(ab), 4);
+            wv = wl(wv, lo32(bb), 5);
+            wv = wl(wv, hi32(bb), 6);
+            wv = wl(wv, lo32(qb), 7);
+            wv = wl(wv, hi32(qb), 8);
+            sel_put<FAST>(grR, b, gtag(seq, t, 0), wv, SEL_NGR);
         }
+        SEL_EV(2);
         SEL_CLK(5);
         // ---- leaving row: the polls go out first, then (while the summaries
         //      travel) the multiplier into its register and to memory
         unsigned w[SEL_NGR];
         SelPoll<SEL_NGR> pr;
         pr.issue(grR, G);
-        if (own) st_x(&Mv[mi(rowsv, li, t)], a, fast);
+        if (own) stx<FAST>(at(Mb + (long long)t * rowsv, moff), a);
         if (b == 0 && lane == 0) {            // read after the launch only (after the publication:
             *gp(&ctlv->c) = C - 1;            // stores pending at a drain delay the summary)
-            *gp(&Mv[mi(rowsv, 0, t)]) = f0;   // row 0's multiplier (+ the sweep's copy)
+            *gp(&Mb[mi(rowsv, 0, t)]) = f0;   // row 0's multiplier (+ the sweep's copy)
             *gp(&MQv[mq(0, t)]) = f0;
         }
         {
-            const int u = t & 15;
-            switch (t >> 4) {
-            case 0: m0[u] = a; break;
-            case 1: m1[u] = a; break;
-            case 2: if constexpr (NK > 2) m2[u] = a; break;
-            default: if constexpr (NK > 3) m3[u] = a; break;
-            }
+            // m<t / 16>[t % 16] = a: every vector takes a select at the index,
+            // in place (a branch per vector made the compiler copy all four)
+            const int u = t & 15, kq = t >> 4;
+            m0[u] = kq == 0 ? a : m0[u];
+            m1[u] = kq == 1 ? a : m1[u];
+            if constexpr (NK > 2) m2[u] = kq == 2 ? a : m2[u];
+            if constexpr (NK > 3) m3[u] = kq == 3 ? a : m3[u];
         }
-        if (!pr.finish(gtag(seq, t, 0), w, &ctlv->bar_timeout, spinv)) {
+        if (!pr.finish(gtag(seq, t, 0), w, &ctlv->bar_timeout, spin)) {
             status = LP_DEVICE_ERROR;
             break;
         }
         SEL_CLK(6);
+        SEL_EV(3);
         const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
-        const double g = wave_min(rl);
+        const double g = wmin(rl);
         long long R = NONE;                   // this device's leaving row (XR: its candidate)
         double aR = 0.0, bR = 0.0;
         if (g < INFINITY) {
@@ -645,9 +728,8 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             const int bs = __builtin_ctzll(__ballot((unsigned)lane < G && rl <= thr));
             aR = rl_d(w[3], w[4], bs);
             bR = rl_d(w[5], w[6], bs);
-            bool okr;
-            const double qr = row_ratio(aR, bR, tol, okr);
-            if (okr && qr <= thr) {
+            const double qR = rl_d(w[7], w[8], bs);
+            if (qR <= thr) {                  // block bs's candidate lies inside the global band
                 R = un_idx(rl32(w[2], bs));
             } else {
                 // rare: block bs's first row inside the global band is not its
@@ -656,16 +738,15 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 if (b == (unsigned)bs) {
                     const int f = __builtin_ctzll(__ballot(okq && q <= thr));
                     const double af = rl_d(lo32(a), hi32(a), f), bf = rl_d(lo32(lcv), hi32(lcv), f);
-                    unsigned wv = 0;
-                    if (lane == 0) wv = (unsigned)(lr0 + f);
-                    else if (lane == 1) wv = lo32(af);
-                    else if (lane == 2) wv = hi32(af);
-                    else if (lane == 3) wv = lo32(bf);
-                    else if (lane == 4) wv = hi32(bf);
-                    sel_put(grS, 0, stag, wv, SEL_NGS, fast);
+                    unsigned wv = (unsigned)(lr0 + f);
+                    wv = wl(wv, lo32(af), 1);
+                    wv = wl(wv, hi32(af), 2);
+                    wv = wl(wv, lo32(bf), 3);
+                    wv = wl(wv, hi32(bf), 4);
+                    sel_put<FAST>(grS, 0, stag, wv, SEL_NGS);
                 }
                 unsigned y[SEL_NGS];
-                if (!sel_gather<SEL_NGS>(grS, 1, stag, y, &ctlv->bar_timeout, spinv)) {
+                if (!sel_gather<SEL_NGS>(grS, 1, stag, y, &ctlv->bar_timeout, spin)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -682,17 +763,22 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         //      local row Rl (stored row, or P[s*] if it was pivot row s* of
         //      this launch, + the later pivots of the launch) / av
         double pv[IPL];
+        double p0 = 0.0;
         auto prow = [&](long long Rl, double avv) {
             const u64 rp = __ballot(lane < t && sRv == Rl);
             const int sst = rp ? 63 - __builtin_clzll(rp) : -1;   // uniform
             // every load issued before any select (see the column's)
+            const double *const xr = Tb + Rl * ld;                 // wave-uniform
+            const double *const mrp = Mb + Rl;
             double x[IPL];
 #pragma unroll
-            for (int k = 0; k < IPL; ++k) x[k] = *gp(Tv + Rl * ld + min(jk[k], (int)nv));
+            for (int k = 0; k < IPL; ++k) x[k] = *gp(at(xr, xoff[k]));
             double mr[NK];
 #pragma unroll
-            for (int k = 0; k < NK; ++k)
-                mr[k] = ld_sc1(&Mv[mi(rowsv, Rl, max(min(16 * k + (lane & 15), t - 1), 0))]);
+            for (int k = 0; k < NK; ++k) mr[k] = ld_sc1(at(mrp, mroff[k]));
+            __builtin_amdgcn_sched_barrier(0);
+            // while the row travels: column 0's pivot value (every block)
+            if constexpr (!XR) p0 = bR / aR;
 #pragma unroll
             for (int k = 0; k < IPL; ++k) x[k] = sst >= 0 ? lP[kc[k] * CS + sst] : (cok[k] ? x[k] : 0.0);
 #pragma unroll
@@ -721,16 +807,15 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             const int N = A.nranks;                 // (a uniform loop bound: kept scalar)
             const unsigned long long xticks = (unsigned long long)A.xwait_ms * 100000ull;
             u64 *xsl = xbufv + par * XS_SUM_PAR;
-            if (b == 0 && lane < SEL_NGR) {
+            if (b == 0 && lane < SEL_NGX) {
                 const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
-                unsigned wv = 0;
-                if (lane == 0) wv = lo32(g);
-                else if (lane == 1) wv = hi32(g);
-                else if (lane == 2) wv = R == NONE ? 0xffffffffu : (unsigned)rglob;
-                else if (lane == 3) wv = lo32(aR);
-                else if (lane == 4) wv = hi32(aR);
-                else if (lane == 5) wv = lo32(bR);
-                else wv = hi32(bR);
+                unsigned wv = R == NONE ? 0xffffffffu : (unsigned)rglob;
+                wv = wl(wv, lo32(g), 0);
+                wv = wl(wv, hi32(g), 1);
+                wv = wl(wv, lo32(aR), 3);
+                wv = wl(wv, hi32(aR), 4);
+                wv = wl(wv, lo32(bR), 5);
+                wv = wl(wv, hi32(bR), 6);
                 for (int p = 0; p < N; ++p)
                     st_sys(&(*gp(peerv + p))[par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
             }
@@ -754,14 +839,14 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 prow(R, aR);
                 send_row(3);
             }
-            unsigned x[SEL_NGR];
+            unsigned x[SEL_NGX];
             const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
-            if (!gather_x<SEL_NGR>(xsl, N, gtag(seq, t, 2), x, &ctlv->bar_timeout, xticks)) {
+            if (!gather_x<SEL_NGX>(xsl, N, gtag(seq, t, 2), x, &ctlv->bar_timeout, xticks)) {
                 status = LP_DEVICE_ERROR;
                 break;
             }
             const double lp = lane < N ? mk_d(x[0], x[1]) : INFINITY;
-            const double gg = wave_min(lp);
+            const double gg = wmin(lp);
             if (!(gg < INFINITY)) {
                 status = LP_UNBOUNDED;
                 break;
@@ -786,22 +871,27 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                     const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
                     u64 *loc = xbufv + XS_PROW + 2LL * N * XS_PROW_RANK;
                     if (lane < SEL_NGS) {
-                        const unsigned wv = lane == 0 ? (mk ? (unsigned)(lr0 + fr) : 0x7fffffffu)
-                                          : lane == 1 ? lo32(ar) : lane == 2 ? hi32(ar)
-                                          : lane == 3 ? lo32(br) : hi32(br);
+                        unsigned wv = mk ? (unsigned)(lr0 + fr) : 0x7fffffffu;
+                        wv = wl(wv, lo32(ar), 1);
+                        wv = wl(wv, hi32(ar), 2);
+                        wv = wl(wv, lo32(br), 3);
+                        wv = wl(wv, hi32(br), 4);
                         st_sc1(&loc[b * 8 + lane], ((u64)gtag(seq, t, 4) << 32) | wv);
                     }
-                    unsigned wl[1][SEL_NGS];
-                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wl, &ctlv->bar_timeout, spinv)) {
+                    unsigned wlo[1][SEL_NGS];
+                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wlo, &ctlv->bar_timeout, spin)) {
                         status = LP_DEVICE_ERROR;
                         break;
                     }
-                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wl[0][0] != 0x7fffffffu));
-                    const unsigned r0w = rl32(wl[0][0], bf), a0 = rl32(wl[0][1], bf), a1 = rl32(wl[0][2], bf),
-                                   b0 = rl32(wl[0][3], bf), b1 = rl32(wl[0][4], bf);
+                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
+                    const unsigned r0w = rl32(wlo[0][0], bf), a0 = rl32(wlo[0][1], bf), a1 = rl32(wlo[0][2], bf),
+                                   b0 = rl32(wlo[0][3], bf), b1 = rl32(wlo[0][4], bf);
                     if (b == 0 && lane < SEL_NGS) {
-                        const unsigned wv = lane == 0 ? (unsigned)((long long)r0w - 1 + rbv)
-                                          : lane == 1 ? a0 : lane == 2 ? a1 : lane == 3 ? b0 : b1;
+                        unsigned wv = (unsigned)((long long)r0w - 1 + rbv);
+                        wv = wl(wv, a0, 1);
+                        wv = wl(wv, a1, 2);
+                        wv = wl(wv, b0, 3);
+                        wv = wl(wv, b1, 4);
                         for (int p = 0; p < N; ++p)
                             st_sys(&(*gp(peerv + p))[par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
                                    ((u64)gtag(seq, t, 5) << 32) | wv);
@@ -847,11 +937,12 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                         status = LP_DEVICE_ERROR;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(SEL_SLEEP);
                 }
                 if (status != LP_PIVOTED) break;
             }
             xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
+            p0 = bR / aR;
         } else {
             prow(R, aR);
         }
@@ -859,25 +950,28 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         //      read from pivot t + 2 on (drained with pivot t + 1's ratio
         //      summary; pivot t + 1 gets P[t][C] with the row-0 summaries);
         //      row 0 is stored once, at the end of the launch
-        const double p0 = bR / aR;
+        {
+            double *const pt = Pb + (long long)t * ld;          // wave-uniform
 #pragma unroll
-        for (int k = 0; k < IPL; ++k)
-            if (cok[k]) st_x(&Pv[t * ld + jk[k]], pv[k], fast);
-        if (b == 0 && lane == 0) *gp(&Pv[t * ld]) = p0;   // read after the launch (sweep)
-        double vn[IPL], vv[IPL], vmin = INFINITY;
+            for (int k = 0; k < IPL; ++k)
+                if (cok[k]) stx<FAST>(at(pt, xoff[k]), pv[k]);
+            if (b == 0 && lane == 0) *gp(pt) = p0;          // read after the launch (sweep)
+        }
+        double vn[IPL], vv[IPL], vmn = INFINITY;
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             vn[k] = upd(0, -1, f0, pv[k], l0v[k]);
             vv[k] = cok[k] ? vn[k] : INFINITY;
-            vmin = fmin(vmin, vv[k]);
+            vmn = fmin(vmn, vv[k]);
         }
         v0 = upd(0, -1, f0, p0, v0);
         double el, eq, epc;
         long long ei, efn;
-        sel_summary<IPL>(vv, pv, vmin, jc0, tol, el, ei, eq, epc, efn);
+        sel_summary<IPL>(vv, pv, vmn, jc0, tol, el, ei, eq, epc, efn);
         const bool more = t + 1 < count;
         const unsigned etag = gtag(seq, t, 1);
-        if (more) sel_put(grE, b, etag, esum_word(el, eq, ei, efn, epc), SEL_NGE, fast);
+        if (more) sel_put<FAST>(grE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
+        SEL_EV(4);
         SEL_CLK(11);
         // ---- while the summaries travel: the pivot-row values into LDS,
         //      column 0 of the own rows (this pivot's multiplier is a), the
@@ -885,50 +979,52 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         SelPoll<SEL_NGE> pe;
         if (more) pe.issue(grE, G);
 #pragma unroll
-            for (int k = 0; k < IPL; ++k) {
-                if (cok[k]) lP[kc[k] * CS + t] = pv[k];
-                l0v[k] = vn[k];
+        for (int k = 0; k < IPL; ++k) {
+            if (cok[k]) lP[kc[k] * CS + t] = pv[k];
+            l0v[k] = vn[k];
+        }
+        if (own) lcv = (li == R) ? p0 : fma(-a, p0, lcv);
+        if (R >= lr0 && R < lr1) {            // uniform: the leaving row is one of this block's
+            if (li == R) {                    // that lane only: its row is P[t] from now on
+                m0 = (d16)0.0;
+                if (t >= 16) m1 = (d16)0.0;
+                if (NK > 2 && t >= 32) m2 = (d16)0.0;
+                if (NK > 3 && t >= 48) m3 = (d16)0.0;
+                pstar = t;
+                arow = Pb + (long long)t * ld;
             }
-            if (own) lcv = (li == R) ? p0 : fma(-a, p0, lcv);
-            if (R >= lr0 && R < lr1) {        // uniform: the leaving row is one of this block's
-                const bool mine = li == R;
-                m0 = mine ? (d16)0.0 : m0;
-                if (t >= 16) m1 = mine ? (d16)0.0 : m1;
-                if (NK > 2 && t >= 32) m2 = mine ? (d16)0.0 : m2;
-                if (NK > 3 && t >= 48) m3 = mine ? (d16)0.0 : m3;
-                if (mine) pstar = t;
-            }
-            if (lane == t) sRv = R;
-            // stall bookkeeping (simplex.py:132-137), min-index switch
-            // (:123,138) and the objective check (:133): every block, from
-            // the same values
-            if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
-                nstd += 1;
-                const double z = -v0;
-                const double band = tol.stall * fmax(1.0, fabs(z0));
-                if (z - z0 > band) stop = 1;
-                if (fabs(z - z0) <= band) stuck += 1;
-                else stuck = 0;
-                if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
-            }
-            if (b == G - 1 && lane < 7) {
-                long long *adr = &dRv[t];
-                long long val = R;
-                if (lane == 1) { adr = &dCv[t]; val = C; }
-                else if (lane == 2) { adr = &ctlv->r; val = rglob; }
-                else if (lane == 3) { adr = &ctlv->npiv; val = npiv + 1; }
-                else if (lane == 4) { adr = &ctlv->ndef[grp]; val = t + 1; }
-                else if (lane == 5) { adr = logv + 2 * min(npiv, logcapv - 1); val = rglob; }
-                else if (lane == 6) { adr = logv + 2 * min(npiv, logcapv - 1) + 1; val = C - 1; }
-                if (lane < 5 || npiv < logcapv) *gp(adr) = val;
-            }
-            if (b == 0 && lane == 0 && mode == MODE_SOLVE) {
-                *gp(&ctlv->nstd) = nstd;
-                *gp(&ctlv->stuck) = stuck;
-                *gp(&ctlv->rule) = rule;
-            }
-            ++npiv;
-            ++ndone;
+        }
+        if (lane == t) sRv = R;
+        // stall bookkeeping (simplex.py:132-137), min-index switch
+        // (:123,138) and the objective check (:133): every block, from
+        // the same values
+        if (mode == MODE_SOLVE && rule == LP_RULE_STANDARD) {
+            nstd += 1;
+            const double z = -v0;
+            const double band = tol.stall * fmax(1.0, fabs(z0));
+            if (z - z0 > band) stop = 1;
+            if (fabs(z - z0) <= band) stuck += 1;
+            else stuck = 0;
+            if (stuck >= A.m + A.n) rule = LP_RULE_MIN_INDEX;
+        }
+        if (b == G - 1 && lane < 7) {
+            long long *adr = &dRv[t];
+            long long val = R;
+            if (lane == 1) { adr = &dCv[t]; val = C; }
+            else if (lane == 2) { adr = &ctlv->r; val = rglob; }
+            else if (lane == 3) { adr = &ctlv->npiv; val = npiv + 1; }
+            else if (lane == 4) { adr = &ctlv->ndef[grp]; val = t + 1; }
+            else if (lane == 5) { adr = logv + 2 * min(npiv, logcapv - 1); val = rglob; }
+            else if (lane == 6) { adr = logv + 2 * min(npiv, logcapv - 1) + 1; val = C - 1; }
+            if (lane < 5 || npiv < logcapv) *gp(adr) = val;
+        }
+        if (b == 0 && lane == 0 && mode == MODE_SOLVE) {
+            *gp(&ctlv->nstd) = nstd;
+            *gp(&ctlv->stuck) = stuck;
+            *gp(&ctlv->rule) = rule;
+        }
+        ++npiv;
+        ++ndone;
         if (!more) {
             if (lane == 0) {                  // the next launch reads plain summaries
                 *gp(&erecv[b].l) = el;
@@ -941,17 +1037,17 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         // ---- the next pivot's entering column
         SEL_CLK(12);
         unsigned we[SEL_NGE];
-        if (!pe.finish(etag, we, &ctlv->bar_timeout, spinv)) {
+        if (!pe.finish(etag, we, &ctlv->bar_timeout, spin)) {
             status = LP_DEVICE_ERROR;
             break;
         }
         SEL_CLK(13);
+        SEL_EV(5);
         rule = __builtin_amdgcn_readfirstlane(rule);
         stop = __builtin_amdgcn_readfirstlane(stop);
         {
             const bool in = (unsigned)lane < G;
             const double el2 = in ? mk_d(we[0], we[1]) : INFINITY;
-            const double eq2 = mk_d(we[2], we[3]);
             const long long ef2 = in ? un_idx(we[5]) : NONE;
             const bool capped = cap >= 0 && npiv >= cap;
             long long Cn = NONE;
@@ -963,7 +1059,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 Cn = wave_min_ll(ef2);
                 if (Cn != NONE) owner = (int)((Cn - 1) / cpb);
             } else {
-                const double g2 = wave_min(el2);
+                const double g2 = wmin(el2);
                 if (g2 < -tol.cost) {
                     ethr = tie_band(g2, tol.cost_tie);
                     const int bs = __builtin_ctzll(__ballot(in && el2 <= ethr));
@@ -1007,16 +1103,15 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                             fv = rl_d(lo32(vn[k]), hi32(vn[k]), lf);
                             pvv = rl_d(lo32(pv[k]), hi32(pv[k]), lf);
                         }
-                    unsigned wv = 0;
-                    if (lane == 0) wv = (unsigned)cc;
-                    else if (lane == 1) wv = lo32(fv);
-                    else if (lane == 2) wv = hi32(fv);
-                    else if (lane == 3) wv = lo32(pvv);
-                    else if (lane == 4) wv = hi32(pvv);
-                    sel_put(grS + 8, 0, atag, wv, SEL_NGS, fast);
+                    unsigned wv = (unsigned)cc;
+                    wv = wl(wv, lo32(fv), 1);
+                    wv = wl(wv, hi32(fv), 2);
+                    wv = wl(wv, lo32(pvv), 3);
+                    wv = wl(wv, hi32(pvv), 4);
+                    sel_put<FAST>(grS + 8, 0, atag, wv, SEL_NGS);
                 }
                 unsigned y[SEL_NGS];
-                if (!sel_gather<SEL_NGS>(grS + 8, 1, atag, y, &ctlv->bar_timeout, spinv)) {
+                if (!sel_gather<SEL_NGS>(grS + 8, 1, atag, y, &ctlv->bar_timeout, spin)) {
                     status = LP_DEVICE_ERROR;
                     break;
                 }
@@ -1024,7 +1119,6 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
                 f0 = rl_d(y[1], y[2], 0);
                 pcw = rl_d(y[3], y[4], 0);
             }
-            (void)eq2;
             C = Cn;
             if (C == NONE) status = stop ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
@@ -1068,6 +1162,71 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         if (stop && status == LP_PIVOTED) status = LP_OBJ_INCREASED;
         if (status != LP_PIVOTED) st_sc1(&ctl->status, status);
     }
+}
+
+}  // namespace
+
+template <int IPL, int NB, bool XR>
+__global__ void __launch_bounds__(GROUP_THREADS)
+k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int first, int fmode, int frule,
+      long long fcap)
+{
+    static_assert(NB % 16 == 0 && NB <= BMAX, "k_sel: pivots per launch");
+    // the grid is 8 x G and only blocks 0, 8, 16, ... work: they share one XCD
+    // under the round-robin dealing of workgroups (checked below)
+    if (blockIdx.x & 7u) return;
+    extern __shared__ __attribute__((aligned(16))) double lP[];   // [cpb][NB + 2]: P[s][own column]
+    const unsigned b = blockIdx.x >> 3, G = (unsigned)gper;
+    const int lane = threadIdx.x;
+    Ctl *const ctl = A.ctl;
+    const bool reset = (first & 1) != 0;
+    if (b == 0 && lane == 0) *gp(&ctl->ndef[grp]) = 0;
+    if (!reset && (ld_sc1(&ctl->status) != LP_PIVOTED || ld_sc1(&ctl->bar_timeout) != 0u)) return;
+    long long npiv = reset ? 0 : ld_sc1(&ctl->npiv);
+    int rule = reset ? frule : ld_sc1(&ctl->rule);
+    long long nstd = 0, stuck = 0;
+    if (!reset) {
+        nstd = ld_sc1(&ctl->nstd);
+        stuck = ld_sc1(&ctl->stuck);
+    }
+    rule = __builtin_amdgcn_readfirstlane(rule);
+    if (lane == 0) {
+        // the loop state before this group: what a timed-out group is redone from
+        st_sc1(&ctl->g_npiv, npiv);
+        st_sc1(&ctl->g_nstd, nstd);
+        st_sc1(&ctl->g_stuck, stuck);
+        st_sc1(&ctl->g_rule, rule);
+        st_sc1(&ctl->g_seq, seq);
+    }
+    {
+        // every block publishes its XCD.  The hand-offs are plain stores that
+        // stay in the XCD's L2, correct only if every block runs there: if not
+        // (never seen), the group is abandoned like a timed-out one and the
+        // host redoes it on the per-pivot kernels (lpgpu.cpp recover_timeout).
+        // (The eager row-0 copies of a call's first launch are drained by its
+        // entering-column exchange, not by this one.)
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        u64 *const grX = A.gran + 2 * GROUP_MAXBLOCKS * GSLOT;
+        drain_stores();
+        if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | xcc);
+        unsigned wx[1];
+        if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
+            if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
+            return;
+        }
+        const bool same = !((unsigned)lane < G) || wx[0] == xcc;
+        if (!__all(same)) {
+            if (b == 0 && lane == 0) {
+                *gp(&ctl->sel_flags) = 8u | 4u;
+                st_sc1(&ctl->bar_timeout, 1u);
+            }
+            return;
+        }
+    }
+    if (b == 0 && lane == 0) *gp(&ctl->sel_flags) = 1u | 4u;   // diagnostics
+    sel_body<IPL, NB, XR, true>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
+                                rule);
 }
 
 // ---- geometry and launch ----------------------------------------------------

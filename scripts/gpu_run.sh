@@ -381,6 +381,20 @@ for step in "$@"; do
             LPGPU_LIB=$L run stamps3_48 300 python scripts/diag_stamps.py mixed 4096 4096 48
             LPGPU_LIB=$L run stamps3_64 300 python scripts/diag_stamps.py mixed 4096 4096 64
             grep -H "^avg\|^pcomp" "$OUT"/stamps3_*.log ;;
+        t3q)
+            # cfg3 quick: one run per pivots-per-sweep value
+            for B in ${T3_BLOCKS:-32 48 64}; do
+                run t3q_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4 --block $B
+            done
+            for f in "$OUT"/t3q_b*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 2))"; done ;;
+        vab)
+            # library variants (make variant NAME=...) on cfg3 at ${VAB_BLOCK:-48} pivots per sweep
+            for V in ${VAB_VARIANTS:-main}; do
+                L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/$V.so
+                [ "$V" = main ] && L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/liblpgpu.so
+                LPGPU_LIB=$L run vab_$V 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4 --block ${VAB_BLOCK:-48}
+            done
+            for f in "$OUT"/vab_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'sel', round(d['selection']['us_per_pivot'], 3))"; done ;;
         r3f)
             run r3f 300 python -u -m pytest tests/test_gpu_r2.py -k timeout -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         clk)

@@ -54,3 +54,31 @@ for k in order:
     tot_mean += mean
     print(f"{names[k]:>12s}  mean {mean:7.0f} cyc {mean / ghz / 1000:5.2f} us   max {max(v):7.0f}   min {min(v):7.0f}")
 print(f"{'sum':>12s}  mean {tot_mean:7.0f} cyc {tot_mean / ghz / 1000:5.2f} us per pivot")
+
+# ---- per-pivot events (100 MHz real-time, 10 ns ticks): where the exchange
+#      waits come from.  Per pivot: spread of the pivot starts over blocks,
+#      the slowest block's column arrival after its start, the spread of the
+#      ratio publications, and how long after the LAST publication each block
+#      saw all of them (the exchange's own latency); the same for row 0.
+EV = 4096
+npv = min(blk, 48)
+rows = []
+for t in range(1, npv - 1):
+    ev = [[buf[EV + (t * 64 + b) * 8 + k] for k in range(6)] for b in range(G)]
+    if any(e[0] == 0 or e[3] == 0 for e in ev):
+        continue
+    s0 = [e[0] for e in ev]
+    col = [e[1] - e[0] for e in ev]
+    p2 = [e[2] for e in ev]
+    seen = [e[3] - max(p2) for e in ev]
+    p4 = [e[4] for e in ev]
+    seen_e = [e[5] - max(p4) for e in ev]
+    rows.append((max(s0) - min(s0), sum(col) / G, max(col), max(p2) - min(p2), min(seen), sum(seen) / G,
+                 max(seen), max(p4) - min(p4), sum(seen_e) / G, max(seen_e)))
+if rows:
+    names_e = ["start spread", "col mean", "col max", "Rpub spread", "Rseen min", "Rseen mean", "Rseen max",
+               "Epub spread", "Eseen mean", "Eseen max"]
+    print("per-pivot events (ns, mean over pivots 1..%d):" % (npv - 2))
+    for i, nm in enumerate(names_e):
+        v = [r[i] * 10.0 for r in rows]
+        print(f"  {nm:>13s} {sum(v) / len(v):8.0f}   max {max(v):8.0f}")
