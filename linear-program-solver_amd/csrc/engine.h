@@ -203,7 +203,7 @@ constexpr int GROUP_MAXBLOCKS = 256;
 constexpr int GRAN_REGIONS = 4;       // regions of Args::gran (see there)
 constexpr int GROUP_MINBLOCKS = 64;    // a small tableau still spreads its columns over 64 blocks
 constexpr int GROUP_THREADS = 64;      // one wave: block reductions stay in registers
-constexpr int GROUP_MAXRPL = 2;        // own rows per lane (<= 64 x 256 x 2 = 32768 rows per device)
+constexpr int GROUP_MAXRPL = 4;        // own rows per lane (<= 64 x 256 x 4 = 65536 rows per device, as LDS allows)
 constexpr long long GROUP_LDS_MAX = 96 * 1024;
 // dynamic LDS of one k_group block: per own row / own column the pivots'
 // values at stride count + 1 (multipliers, pivot-row values) + row 0 /

@@ -1951,6 +1951,223 @@ k_sweep_dp2(const double *T, double *Tout, const double *__restrict__ P, const d
     }
 }
 
+// ---------------------------------------------------------------------------
+// The register-operand FMA block of k_sweep_rl (below): 16 FMAs of pivots 2c,
+// 2c + 1 on a batch's 8 rows, one column per lane, the pivot-row values in
+// plain VGPRs and the multiplier read with a row_newbcast DPP operand from
+// lane 8h + k of the lane's 16-lane row:
+//     v_fmac_f64_dpp x[k], -m[c], p[2c + h] row_newbcast:(8h + k)
+// ---------------------------------------------------------------------------
+#define RGF(XK, P, L) "v_fmac_f64_dpp %" #XK ", -%8, %" #P " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
+#define RG_OUTS(x) "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+// pivots 2c, 2c + 1 on the batch's 8 rows
+__device__ __forceinline__ void rg_pair(double (&x)[8], double m, double pa, double pb)
+{
+    asm("s_nop 1\n" RGF(0, 9, 0) RGF(1, 9, 1) RGF(2, 9, 2) RGF(3, 9, 3) RGF(4, 9, 4) RGF(5, 9, 5) RGF(6, 9, 6)
+            RGF(7, 9, 7) RGF(0, 10, 8) RGF(1, 10, 9) RGF(2, 10, 10) RGF(3, 10, 11) RGF(4, 10, 12) RGF(5, 10, 13)
+                RGF(6, 10, 14) RGF(7, 10, 15)
+        : RG_OUTS(x) : "v"(m), "v"(pa), "v"(pb));
+}
+#undef RG_OUTS
+#undef RGF
+
+// ---------------------------------------------------------------------------
+// K3 (registers + LDS streaming): k_sweep_rl (LPGPU_SWEEP_DP=5, A/B).  The
+//   DPP sweeps above read P from LDS for every pivot of every batch (16 bytes
+//   per lane per 8 FMAs: more LDS bandwidth per FMA than a CU has at full
+//   FMA rate).  Here the pivot rows stay in registers and no operand of an FMA
+//   comes from LDS: the tableau rows and the multipliers travel HBM -> LDS
+//   with global_load_lds_dwordx4 (no VGPRs), D batches deep, and each batch is
+//   read into registers once:
+//     * a workgroup of W waves owns a strip of 64 W columns (one per lane) of a
+//       run of rows; all W waves take the SAME 8-row batch, each on its own 64
+//       columns, so the batch's multipliers (two MQ quads, 4 KB) are copied
+//       once per workgroup -- one dwordx4 per wave;
+//     * each wave keeps P[0..NB) of its column in registers;
+//     * per batch: wait for its copies (vmcnt, one workgroup barrier), start the
+//       copies of batch i + D - 1 into the slot batch i - 1 used, read x (8
+//       rows) and the multipliers' DPP registers from LDS, the FMAs, store x.
+//   Every element gets exactly upd()'s float64 operations in pivot order:
+//   bit-identical to oracle/lp_f64.c (the GPU suite passes with it).
+//   Measured (cfg3, profiles/r03/README.md): no faster than k_sweep_dp /
+//   k_sweep_dp2 (151.7 against 149.7 us at 64 pivots, 118.3 against 113.2 at
+//   48; scripts/fma_probe.hip rules out the FMA issue rate: 55 TFLOP/s at two
+//   waves per SIMD), so the DPP sweeps stay the default.  (A first version
+//   with the rows in VGPRs, one batch in flight per wave, reached 0.41 of HBM.)
+// ---------------------------------------------------------------------------
+// LDS byte offset of a __shared__ location (for LDS accesses written in asm)
+__device__ __forceinline__ unsigned lds_off(const double *p)
+{
+    return (unsigned)(unsigned long)(const __attribute__((address_space(3))) double *)p;
+}
+// k_sweep_rl's rows: x[k] = LDS[a + 512 k]
+template <int RW>
+__device__ __forceinline__ void lds_rows(double (&x)[RW], unsigned a)
+{
+    static_assert(RW == 8, "lds_rows");
+    asm volatile("ds_read_b64 %0, %8\n ds_read_b64 %1, %8 offset:512\n ds_read_b64 %2, %8 offset:1024\n"
+                 "ds_read_b64 %3, %8 offset:1536\n ds_read_b64 %4, %8 offset:2048\n ds_read_b64 %5, %8 offset:2560\n"
+                 "ds_read_b64 %6, %8 offset:3072\n ds_read_b64 %7, %8 offset:3584"
+                 : "=v"(x[0]), "=v"(x[1]), "=v"(x[2]), "=v"(x[3]), "=v"(x[4]), "=v"(x[5]), "=v"(x[6]), "=v"(x[7])
+                 : "v"(a));
+}
+// k_sweep_rl's multiplier registers: m[c] = LDS[a + 64 c]
+template <int C>
+__device__ __forceinline__ void lds_mult_one(double &m, unsigned a)
+{
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(m) : "v"(a), "n"(64 * C));
+}
+template <int NC, int C = 0>
+__device__ __forceinline__ void lds_mult(double (&m)[NC], unsigned a)
+{
+    if constexpr (C < NC) {
+        lds_mult_one<C>(m[C], a);
+        lds_mult<NC, C + 1>(m, a);
+    }
+}
+
+template <int W, int NB, int D, int SA>
+__global__ void __launch_bounds__(64 * W)
+k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
+           const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
+           int nstrips, long long run)
+{
+    constexpr int RW = 8;                        // rows per batch
+    constexpr int NC = NB / 2;                   // multiplier registers (2 pivots x 8 rows each)
+    constexpr int XS = W * RW * 64;              // doubles of a slot's rows (W waves x 8 rows x 64 columns)
+    constexpr int MS = 2 * 4 * BMAX;             // doubles of a slot's multipliers (two MQ quads)
+    static_assert(NB % 2 == 0 && NB <= BMAX && D >= 2 && W >= 4, "k_sweep_rl");
+    __shared__ __attribute__((aligned(16))) double xs[D][XS];
+    __shared__ __attribute__((aligned(16))) double ms[D][MS];
+    __shared__ long long sr[NB];
+    const int nd = (int)ctl->ndef[grp];
+    if (nd == 0 || ctl->bar_timeout) return;     // nothing deferred / group redone by the host
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
+    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
+    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
+    const long long r1 = min(rows, r0 + run);
+    // this lane's column.  Lanes past the pitch (the last strip of a pitch
+    // that is not a multiple of 64 W) take the column their LDS position was
+    // copied from (ld - 2 or ld - 1) and store the same values as its owner,
+    // so every wave issues the same instructions (the waits count them)
+    const long long colw = (long long)strip * 64 * W + 64 * wave;
+    const long long col = min(colw + (lane & ~1), ld - 2) + (lane & 1);
+    const bool cok = colw + lane < ld;
+    if (nd != NB) {
+        // a partial group (a call's last, or a stop inside it): pivot by
+        // pivot from memory -- rare, never on the timed path
+        __syncthreads();
+        for (long long row = r0; row < r1; ++row) {
+            double x = T[row * ld + col];
+            for (int s = 0; s < nd; ++s) {
+                if (sr[s] == row) x = P[(long long)s * ld + col];      // the pivot row becomes P[s]
+                else x = fma(-M[mq(row, s)], P[(long long)s * ld + col], x);
+            }
+            if (cok) Tout[row * ld + col] = x;
+        }
+        return;
+    }
+    double p[NB];
+#pragma unroll
+    for (int s = 0; s < NB; ++s) p[s] = P[(long long)s * ld + col];
+    const long long nbat = (r1 - r0 + RW - 1) / RW;
+    const long long nquad = (rows + 3) >> 2;
+    // copies of batch i into slot i % D: lane l of a wave brings 16 bytes --
+    // rows: row 2 q + (l >> 5) of the wave's 8, columns 2 (l & 31) .. +1 of
+    // its 64, for q = 0..3 (4 instructions); multipliers: quad (wave >> 1) of
+    // the batch, bytes 1 KB x (wave & 1) + 16 l of it (one instruction)
+    auto issue = [&](long long i) {
+        const int slot = (int)(i % D);
+        const long long rb = r0 + i * RW;
+        const long long last = r1 - 1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const long long row = min(rb + 2 * q + (lane >> 5), last);
+            const long long cc = min(colw + 2 * (lane & 31), ld - 2);
+            __builtin_amdgcn_global_load_lds(T + row * ld + cc,
+                                             (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
+                                             16, 0, 0);
+        }
+        // (W >= 4: quads 0, 1 x halves 0, 1 by waves 0..3; more waves re-copy)
+        const int w4 = wave & 3;
+        const long long qd = min((rb >> 2) + (w4 >> 1), nquad - 1);
+        __builtin_amdgcn_global_load_lds(M + qd * (4 * BMAX) + (w4 & 1) * 128 + 2 * lane,
+                                         (__attribute__((address_space(3))) void *)&ms[slot][(w4 >> 1) * (4 * BMAX) + (w4 & 1) * 128],
+                                         16, 0, 0);
+    };
+    // vector-memory instructions a wave issues per batch after the copies of
+    // batch i: the copies of the next batches (5 each) and the stores (8 each)
+    constexpr int PER = 5 + RW;
+    __syncthreads();                             // sr staged
+#pragma unroll 1
+    for (long long i = 0; i < D - 1; ++i) issue(i);
+    const int vh = (lane & 15) >> 3, vk = lane & 7;
+#pragma unroll 1
+    for (long long i = 0; i < nbat; ++i) {
+        // batch i's copies are the oldest outstanding but for the D - 2 later
+        // batches' copies and stores issued since (the copies of the last
+        // batches are issued anyway, re-reading the last one)
+        // (the first D - 1 batches: fewer issued since -- the prologue's
+        // copies have no stores between them)
+        static_assert(D <= 4, "k_sweep_rl: waits written for D <= 4");
+        if (i >= D - 1) {
+            if constexpr (D == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + PER) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + 2 * PER) : "memory");
+        } else if (i == 0) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 5) : "memory");
+        } else if (i == 1) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D == 3 ? PER : 5 + PER) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");   // D == 4, i == 2
+        }
+        __syncthreads();                         // every wave's copies of batch i are in LDS
+        issue(min(i + D - 1, nbat - 1));         // into the slot batch i - 1 used (all waves past it)
+        const int slot = (int)(i % D);
+        const long long rb = r0 + i * RW;
+        const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
+        double x[RW], m[NC];
+        // multiplier of pivot 2c + h, batch row k (past kmax: row kmax's)
+        const int kr = min(vk, kmax);
+        if (kmax == RW - 1) {
+            // the LDS reads in asm: a compiler-visible read of LDS the copies
+            // write made it wait for every copy in flight (vmcnt(0)) first;
+            // the wait above already covers this batch's
+            const unsigned xa = lds_off(&xs[slot][wave * RW * 64 + lane]);
+            const unsigned ma = lds_off(&ms[slot][(kr >> 2) * (4 * BMAX) + (kr & 3) + vh * 4]);
+            lds_rows<RW>(x, xa);
+            lds_mult<NC>(m, ma);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else {
+#pragma unroll
+            for (int k = 0; k < RW; ++k) x[k] = xs[slot][(wave * RW + min(k, kmax)) * 64 + lane];
+            const double *mrow = &ms[slot][(kr >> 2) * (4 * BMAX) + (kr & 3)];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) m[c] = mrow[(2 * c + vh) * 4];
+        }
+#pragma unroll
+        for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
+#pragma unroll
+        for (int k = 0; k < RW; ++k) Tout[(rb + min(k, kmax)) * ld + col] = x[k];
+    }
+    // the group's pivot rows in this run: recomputed after the pass (rare)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int s0 = 0; s0 < nd; ++s0) {
+        const long long row = sr[s0];
+        if (row < r0 || row >= r1) continue;     // block-uniform
+        double y = p[0];
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            if (s == s0) y = p[s];
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            if (s > s0) y = fma(-M[mq(row, s)], p[s], y);
+        if (cok) Tout[row * ld + col] = y;
+    }
+}
+
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
 // into rank p's summary slot, then every lane waits for rank p's granule in
 // the local buffer (bounded)
@@ -2228,11 +2445,40 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
     constexpr int W = 8, RW = 4, SA = 16;
     // LPGPU_SWEEP_DP (A/B): 1 (default) k_sweep_dp2 up to 48 pivots per sweep and
     // k_sweep_dp at 64 (cfg3 B = 48: 119 against 126-128 us; cfg4 B = 64: 1083-1089
-    // against 1093-1096 us), 2 k_sweep_dp2 always, 3 k_sweep_dp always, 0 k_sweep_st
+    // against 1093-1096 us), 2 k_sweep_dp2 always, 3 k_sweep_dp always, 0 k_sweep_st,
+    // 5 k_sweep_rl (pivot rows in registers, rows streamed through LDS)
     static int dpp = -1;
     if (dpp < 0) {
         const char *v = std::getenv("LPGPU_SWEEP_DP");
         dpp = v ? std::atoi(v) : 1;
+    }
+    if (dpp == 5 && A.ld % 64 == 0 && A.ld >= 128) {
+        // k_sweep_rl: 256-column strips, pivot rows in registers, rows and
+        // multipliers streamed into LDS three batches deep
+        constexpr int WL = 4, DL = 3;
+        const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
+        const void *fn = nb == 16 ? (const void *)&k_sweep_rl<WL, 16, DL, SA>
+                       : nb == 32 ? (const void *)&k_sweep_rl<WL, 32, DL, SA>
+                       : nb == 48 ? (const void *)&k_sweep_rl<WL, 48, DL, SA>
+                                  : (const void *)&k_sweep_rl<WL, 64, DL, SA>;
+        const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
+        const long long nsg = (A.ld + 64 * WL - 1) / (64 * WL);
+        const long long slots = (long long)sweep_cus() * bpc;
+        long long nrun = slots / nsg;
+        if (nrun < 1) nrun = 1;
+        long long run = (A.rows + nrun - 1) / nrun;
+        run = (run + 7) / 8 * 8;                 // whole 8-row batches (the multipliers' quads)
+        nrun = (A.rows + run - 1) / run;
+        const dim3 grid((unsigned)(nrun * nsg));
+        const double *T = A.T, *Pp = A.P, *Mp = A.MQ;
+        double *To = A.T;
+        const long long *dRp = A.dR;
+        const Ctl *ctlp = A.ctl;
+        long long ld = A.ld, rows = A.rows;
+        int grpv = grp, nsv = (int)nsg;
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run};
+        const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
+        return err != hipSuccess ? err : hipGetLastError();
     }
     const long long ns = (A.ld + 127) / 128;
     if (dpp) {
@@ -2318,7 +2564,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
 // ---- k_group geometry and launch ------------------------------------------
 // compiled variants (summaries per lane, columns per lane, rows per lane)
 #define GROUP_VARIANTS(X) \
-    X(1, 2, 1) X(2, 2, 1) X(4, 2, 1) X(1, 3, 1) X(2, 3, 1) X(1, 4, 1) X(2, 4, 1) X(4, 4, 1) X(4, 2, 2) X(4, 4, 2)
+    X(1, 2, 1) X(2, 2, 1) X(4, 2, 1) X(1, 3, 1) X(2, 3, 1) X(1, 4, 1) X(2, 4, 1) X(4, 4, 1) X(4, 2, 2) X(4, 4, 2) \
+        X(4, 2, 4) X(4, 4, 4)
 
 static const void *group_kernel(int nr, int ipl, int rpl, bool xr, bool hk = false)
 {
@@ -2392,7 +2639,7 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, in
     };
     Cand cand[2 * GROUP_MAXRPL];
     int nc = 0;
-    for (int rpl = 1; rpl <= GROUP_MAXRPL; ++rpl)
+    for (int rpl = 1; rpl <= GROUP_MAXRPL; rpl *= 2)   // compiled: 1, 2, 4 rows per lane
         for (int wide = 1; wide >= 0; --wide) {
             long long g = (rc + 64LL * rpl - 1) / (64LL * rpl);
             if (g < GROUP_MINBLOCKS) g = GROUP_MINBLOCKS;
@@ -2432,7 +2679,7 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, in
             nr = nr <= 1 ? 1 : nr <= 2 ? 2 : 4;
             int ipl = (int)((cpb + GROUP_THREADS - 1) / GROUP_THREADS);
             ipl = ipl <= 2 ? 2 : (ipl == 3 && nr <= 2) ? 3 : 4;
-            if (rpl == 2) {
+            if (rpl >= 2) {
                 nr = 4;
                 ipl = ipl <= 2 ? 2 : 4;
             }

@@ -230,6 +230,9 @@ __device__ __forceinline__ void row_chain(double (&x)[IPL], const double (&mr)[N
 // immediate offset (the per-granule addresses of the general layout, kept
 // live across the pivot loop, cost k_sel about 70 VGPRs).
 constexpr int SEL_SLOT = 64;
+#ifndef SEL_PIPE
+#define SEL_PIPE 0             // exchanges keep two polls in flight
+#endif
 #ifndef SEL_SLEEP
 #define SEL_SLEEP 1            // s_sleep between the polls of an exchange (64 clocks per unit)
 #endif
@@ -387,33 +390,62 @@ template <int NG>
 struct SelPoll {
     const u64 *p;
     u64 v[NG];
+#if SEL_PIPE
+    u64 u[NG];
+#endif
+    __device__ __forceinline__ void load(u64 (&d)[NG])
+    {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) d[g] = ld_sc1(p + g * SEL_SLOT);
+    }
+    __device__ __forceinline__ bool take(unsigned tag, const u64 (&d)[NG], unsigned (&w)[NG])
+    {
+        bool ok = true;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            w[g] = (unsigned)d[g];
+            ok = ok && (unsigned)(d[g] >> 32) == tag;
+        }
+        return __all(ok);
+    }
     __device__ __forceinline__ void issue(const u64 *base, unsigned G)
     {
         p = base + min((unsigned)threadIdx.x, G - 1);
-#pragma unroll
-        for (int g = 0; g < NG; ++g) v[g] = ld_sc1(p + g * SEL_SLOT);
+        load(v);
+#if SEL_PIPE
+        load(u);
+#endif
         __builtin_amdgcn_sched_barrier(0);
     }
     __device__ __forceinline__ bool finish(unsigned tag, unsigned (&w)[NG], unsigned *timeout_flag,
                                            unsigned spin_max)
     {
         __builtin_amdgcn_sched_barrier(0);
-        for (unsigned spins = 0;; ++spins) {
-            bool ok = true;
-#pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                w[g] = (unsigned)v[g];
-                ok = ok && (unsigned)(v[g] >> 32) == tag;
+#if SEL_PIPE
+        // two polls always in flight: the older one is checked while the
+        // newer one travels, and a new one goes out behind it (unrolled by
+        // two so that no register copy waits for a load in flight)
+        for (unsigned spins = 0;; spins += 2) {
+            if (take(tag, v, w)) return true;
+            load(v);
+            if (take(tag, u, w)) return true;
+            load(u);
+            if (spins > spin_max) {
+                st_sc1(timeout_flag, 1u);
+                return false;
             }
-            if (__all(ok)) return true;
+        }
+#else
+        for (unsigned spins = 0;; ++spins) {
+            if (take(tag, v, w)) return true;
             if (spins > spin_max) {
                 st_sc1(timeout_flag, 1u);
                 return false;
             }
             __builtin_amdgcn_s_sleep(SEL_SLEEP);
-#pragma unroll
-            for (int g = 0; g < NG; ++g) v[g] = ld_sc1(p + g * SEL_SLOT);
+            load(v);
         }
+#endif
     }
 };
 
@@ -421,6 +453,26 @@ constexpr int SEL_NGR = 9;   // ratio summary: l (2), i, a (2), b (2), q of the 
 constexpr int SEL_NGE = 8;   // row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
 constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
 constexpr int SEL_NGX = 7;   // XR rank summary: l (2), global row, a (2), b (2)
+
+// pivot TQ's deferred register work (sel_body): its multiplier into m<TQ / 16>
+// [TQ % 16] -- every vector takes a select at the index, in place (a branch
+// per vector made the compiler copy all four) -- and to M; the multipliers of
+// its leaving row zeroed (fma(-p, 0, x) == x: that row is P[TQ] from then on)
+#define SEL_SETTLE(TQ)                                                                              \
+    do {                                                                                            \
+        const int tq_ = (TQ), u_ = tq_ & 15, kq_ = tq_ >> 4;                                        \
+        m0[u_] = kq_ == 0 ? apend : m0[u_];                                                         \
+        m1[u_] = kq_ == 1 ? apend : m1[u_];                                                         \
+        if constexpr (NK > 2) m2[u_] = kq_ == 2 ? apend : m2[u_];                                   \
+        if constexpr (NK > 3) m3[u_] = kq_ == 3 ? apend : m3[u_];                                   \
+        if (own) stx<FAST>(at(Mb + (long long)tq_ * rowsv, moff), apend);                           \
+        if (zpend) {                                                                                \
+            m0 = (d16)0.0;                                                                          \
+            if (tq_ >= 16) m1 = (d16)0.0;                                                           \
+            if (NK > 2 && tq_ >= 32) m2 = (d16)0.0;                                                 \
+            if (NK > 3 && tq_ >= 48) m3 = (d16)0.0;                                                 \
+        }                                                                                           \
+    } while (0)
 
 // The pivot loop of k_sel.  NB: most pivots of a launch (register
 // multipliers); IPL: own columns per lane (cpb <= 64 IPL); XR: one rank of a
@@ -545,6 +597,11 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     // this lane's row: the multiplier of pivot s in m<s / 16>[s % 16]
     d16 m0 = (d16)0.0, m1 = (d16)0.0, m2 = (d16)0.0, m3 = (d16)0.0;
     int pstar = -1;                             // the latest pivot of the launch whose row was the lane's
+    // the previous pivot's register work, done while the next column travels:
+    // its multiplier of the lane's row (apend) into m and to M, and -- in the
+    // lane holding its leaving row (zpend) -- that row's multipliers zeroed
+    double apend = 0.0;
+    bool zpend = false;
     long long sRv = -1;                         // lane s: pivot s's local row (-1: another rank's)
     int status = LP_PIVOTED;
     int stop = 0;                               // the objective increased (simplex.py:133)
@@ -643,6 +700,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         const unsigned pkc = (unsigned)max(t - 2, 0) * (unsigned)ld * 8u;
 #pragma unroll
         for (int k = 0; k < NK; ++k) pk[k] = ld_sc1(at(cP, 16 * k + (lane & 15) <= t - 2 ? pkoff[k] : pkc));
+        if (t > 0) SEL_SETTLE(t - 1);
         const bool apcw = pstar >= 0 && pstar == t - 1;
         a = own ? (apcw ? pcw : a) : 0.0;
 #pragma unroll
@@ -698,20 +756,11 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         unsigned w[SEL_NGR];
         SelPoll<SEL_NGR> pr;
         pr.issue(grR, G);
-        if (own) stx<FAST>(at(Mb + (long long)t * rowsv, moff), a);
+        apend = a;
         if (b == 0 && lane == 0) {            // read after the launch only (after the publication:
             *gp(&ctlv->c) = C - 1;            // stores pending at a drain delay the summary)
             *gp(&Mb[mi(rowsv, 0, t)]) = f0;   // row 0's multiplier (+ the sweep's copy)
             *gp(&MQv[mq(0, t)]) = f0;
-        }
-        {
-            // m<t / 16>[t % 16] = a: every vector takes a select at the index,
-            // in place (a branch per vector made the compiler copy all four)
-            const int u = t & 15, kq = t >> 4;
-            m0[u] = kq == 0 ? a : m0[u];
-            m1[u] = kq == 1 ? a : m1[u];
-            if constexpr (NK > 2) m2[u] = kq == 2 ? a : m2[u];
-            if constexpr (NK > 3) m3[u] = kq == 3 ? a : m3[u];
         }
         if (!pr.finish(gtag(seq, t, 0), w, &ctlv->bar_timeout, spin)) {
             status = LP_DEVICE_ERROR;
@@ -984,15 +1033,10 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             l0v[k] = vn[k];
         }
         if (own) lcv = (li == R) ? p0 : fma(-a, p0, lcv);
-        if (R >= lr0 && R < lr1) {            // uniform: the leaving row is one of this block's
-            if (li == R) {                    // that lane only: its row is P[t] from now on
-                m0 = (d16)0.0;
-                if (t >= 16) m1 = (d16)0.0;
-                if (NK > 2 && t >= 32) m2 = (d16)0.0;
-                if (NK > 3 && t >= 48) m3 = (d16)0.0;
-                pstar = t;
-                arow = Pb + (long long)t * ld;
-            }
+        zpend = li == R;                      // that lane only: its row is P[t] from now on
+        if (zpend) {
+            pstar = t;
+            arow = Pb + (long long)t * ld;
         }
         if (lane == t) sRv = R;
         // stall bookkeeping (simplex.py:132-137), min-index switch
@@ -1138,6 +1182,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     // the launch
     {
         const int nds = __builtin_amdgcn_readfirstlane(ndone);
+        if (nds > 0) SEL_SETTLE(nds - 1);
 #pragma unroll
         for (int s = 0; s < NB; ++s)
             if (s < nds && own) {

@@ -392,16 +392,30 @@ for step in "$@"; do
             for V in ${VAB_VARIANTS:-main}; do
                 L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/$V.so
                 [ "$V" = main ] && L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/liblpgpu.so
-                LPGPU_LIB=$L run vab_$V 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4 --block ${VAB_BLOCK:-48}
+                LPGPU_LIB=$L run vab_$V 300 python bench.py --no-cpu-baseline --workload ${VAB_WORKLOAD:-cfg3} --steps 64 --warmup 4 --block ${VAB_BLOCK:-48}
             done
             for f in "$OUT"/vab_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'sel', round(d['selection']['us_per_pivot'], 3))"; done ;;
+        rgtest)
+            LPGPU_SWEEP_DP=${SWV:-4} run rgtest 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        rgab)
+            for B in ${T3_BLOCKS:-32 48 64}; do
+                run rgab_def_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4 --block $B
+                LPGPU_SWEEP_DP=${SWV:-4} run rgab_rg_b$B 300 python bench.py --no-cpu-baseline --workload cfg3 --steps 64 --warmup 4 --block $B
+            done
+            for f in "$OUT"/rgab_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 3))"; done ;;
+        r3new)
+            run r3new 900 python -u -m pytest tests/test_gpu_r3.py -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "40000" ;;
+        r3procs)
+            run r3procs 1000 python -u -m pytest tests/test_gpu_r3_procs.py -v -p no:cacheprovider --timeout 900 --timeout-method thread ;;
         r3f)
             run r3f 300 python -u -m pytest tests/test_gpu_r2.py -k timeout -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         clk)
-            L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/stamps.so
-            for B in ${CLK_BLOCKS:-48}; do
-                LPGPU_LIB=$L run clk_b$B 300 python scripts/sel_clocks.py mixed 4096 4096 $B
-                cat "$OUT/clk_b$B.log"
+            for V in ${CLK_VARIANTS:-stamps}; do
+                L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/$V.so
+                for B in ${CLK_BLOCKS:-48}; do
+                    LPGPU_LIB=$L run clk_${V}_b$B 300 python scripts/sel_clocks.py mixed 4096 4096 $B
+                    cat "$OUT/clk_${V}_b$B.log"
+                done
             done ;;
         r3p)
             run r3p 600 python -u -m pytest tests/test_gpu_r3.py -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;

@@ -202,8 +202,8 @@ def test_optimal_at_start_and_cap():
     ("tall", 1, 1, 3), ("mixed", 1, 5, 3), ("mixed", 3, 60, 10), ("tall", 5, 63, 10),
     ("tall", 257, 64, 30), ("mixed", 300, 191, 30), ("tall", 513, 7, 20),
     ("tall", 1000, 2, 10), ("tall", 2, 5000, 10), ("mixed", 255, 129, 40),
-    # two rows per lane (> 256 blocks x 64 rows), the 32768-row limit, past it
-    # (per-pivot kernels), past 256 x 256 columns
+    # two rows per lane (> 256 blocks x 64 rows), 32768 rows, past it (four
+    # rows per lane since round 3), past 256 x 256 columns
     ("tall", 16500, 3, 12), ("tall", 32768, 9, 8), ("tall", 32769, 3, 6), ("tall", 2, 66000, 6),
 ])
 @pytest.mark.parametrize("block", [1, 7, 32, 48])

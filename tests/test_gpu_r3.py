@@ -189,3 +189,20 @@ def test_two_level_objective_increased():
     geo = e.geometry()
     assert geo["kernel"] == "k_group" and geo["two_level_engaged"], geo
     e.close()
+
+
+def test_tall_40000_rows_persistent():
+    """the persistent selection past 32768 rows per device (four
+    own rows per lane): a 40000 x 64 tall tableau stays on PATH_PERSISTENT,
+    150 pivots bit-exact (auto pivots per sweep and 64)"""
+    T = gen.tableau("tall", 40000, 64, 5)
+    o = F64Tableau(T)
+    ost, olog = o.run(0, 150)
+    for block in (0, 64):
+        e = _engine(T, block)
+        st, done = e.run(_lib.RULE_STANDARD, 150)
+        assert e.exchange_path() == (_lib.PATH_PERSISTENT, 0)
+        assert e.geometry()["rpl"] == 4, e.geometry()
+        assert e.log().tolist() == olog.tolist()
+        assert np.array_equal(e.download(), o.T)
+        e.close()
