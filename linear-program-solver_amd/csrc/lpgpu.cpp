@@ -672,8 +672,12 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     h->share = 1;
     while (h->share < 8 && (bits >> h->share)) ++h->share;
     h->xr_xcd = h->share == 1;
-    if (const char *v = std::getenv("LPGPU_XR_XCD")) {   // A/B and tests: 0 off
+    if (const char *v = std::getenv("LPGPU_XR_XCD")) {
+        // A/B and tests: 0 off; 1 on even for ranks sharing a GPU (tests of
+        // the one-XCD cross-rank selection k_sel<XR> on one box: small
+        // tableaux, whose ranks' blocks all fit on the one XCD together)
         if (v[0] == '0') h->xr_xcd = false;
+        if (v[0] == '1') h->xr_xcd = true;
     }
     return LP_PIVOTED;
 }
@@ -929,7 +933,7 @@ static lpk::GroupGeom persistent_geom_b(lp_handle *h, size_t nmem, int *xr, int 
     if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
     *xr = (nmem == 1 && h->xr_xcd) ? 2 : 1;
-    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 ? h->share : 1);
+    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 && *xr != 2 ? h->share : 1);
 }
 
 // Pivots per sweep when the handle says auto (0).  More pivots per sweep cut

@@ -110,15 +110,25 @@ template <int NK>
 __device__ __forceinline__ void col_chain(double &a, const double (&pk)[NK], const d16 &m0, const d16 &m1,
                                           const d16 &m2, const d16 &m3, int t)
 {
-    if (t > 0) col_chunk<NK, 0>(a, pk[0], m0);
-    if (t > 8) col_chunk<NK, 1>(a, pk[0], m0);
-    if (t > 16) col_chunk<NK, 2>(a, pk[1], m1);
-    if (t > 24) col_chunk<NK, 3>(a, pk[1], m1);
+    // (the first chunk past t ends the chain: one taken branch, not one per
+    // remaining chunk)
+    if (t <= 0) return;
+    col_chunk<NK, 0>(a, pk[0], m0);
+    if (t <= 8) return;
+    col_chunk<NK, 1>(a, pk[0], m0);
+    if (t <= 16) return;
+    col_chunk<NK, 2>(a, pk[1], m1);
+    if (t <= 24) return;
+    col_chunk<NK, 3>(a, pk[1], m1);
     if constexpr (NK > 2) {
-        if (t > 32) col_chunk<NK, 4>(a, pk[2], m2);
-        if (t > 40) col_chunk<NK, 5>(a, pk[2], m2);
-        if (t > 48) col_chunk<NK, 6>(a, pk[3], m3);
-        if (t > 56) col_chunk<NK, 7>(a, pk[3], m3);
+        if (t <= 32) return;
+        col_chunk<NK, 4>(a, pk[2], m2);
+        if (t <= 40) return;
+        col_chunk<NK, 5>(a, pk[2], m2);
+        if (t <= 48) return;
+        col_chunk<NK, 6>(a, pk[3], m3);
+        if (t <= 56) return;
+        col_chunk<NK, 7>(a, pk[3], m3);
     }
 }
 #undef SEL_COL8
@@ -271,12 +281,12 @@ __device__ __forceinline__ void stx(T *p, T v)
 }
 
 // minimum of two doubles as v_min_f64 computes it, without the NaN
-// canonicalisation fmin() adds (no operand here is a NaN); the s_nop covers
-// the two wait states a DPP read of the result needs after this VALU write
+// canonicalisation fmin() adds (no operand here is a NaN).  (The compiler
+// puts the two wait states a DPP read of the result needs after it.)
 __device__ __forceinline__ double vmin(double a, double b)
 {
     double r;
-    asm("v_min_f64 %0, %1, %2\n\ts_nop 1" : "=v"(r) : "v"(a), "v"(b));
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
 template <int CTRL, int RM>
@@ -635,7 +645,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
 #pragma unroll
                 for (int k = 0; k < IPL; ++k) {
                     vv[k] = cok[k] ? l0v[k] : INFINITY;
-                    vmn = fmin(vmn, vv[k]);
+                    vmn = vmin(vmn, vv[k]);
                     pz[k] = 0.0;
                 }
                 double sel_, seq_, spc_;
@@ -1011,7 +1021,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         for (int k = 0; k < IPL; ++k) {
             vn[k] = upd(0, -1, f0, pv[k], l0v[k]);
             vv[k] = cok[k] ? vn[k] : INFINITY;
-            vmn = fmin(vmn, vv[k]);
+            vmn = vmin(vmn, vv[k]);
         }
         v0 = upd(0, -1, f0, p0, v0);
         double el, eq, epc;

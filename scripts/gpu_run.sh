@@ -406,7 +406,7 @@ for step in "$@"; do
         r3new)
             run r3new 900 python -u -m pytest tests/test_gpu_r3.py -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "40000" ;;
         r3procs)
-            run r3procs 1000 python -u -m pytest tests/test_gpu_r3_procs.py -v -p no:cacheprovider --timeout 900 --timeout-method thread ;;
+            run r3procs 1000 python -u -m pytest tests/test_gpu_r3_procs.py -v -p no:cacheprovider --timeout 900 --timeout-method thread ${R3P_K:+-k "$R3P_K"} ;;
         r3f)
             run r3f 300 python -u -m pytest tests/test_gpu_r2.py -k timeout -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         clk)

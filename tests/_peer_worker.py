@@ -47,6 +47,9 @@ def main():
     # ranks on the one GPU, one collective per pivot beyond (lpgpu.cpp,
     # persistent_geom) or without the peer exchange
     path, fallbacks = e.exchange_path()
+    if os.environ.get("EXPECT_KERNEL"):        # which selection kernel the persistent path ran
+        geo = e.geometry()
+        assert geo["kernel"] == os.environ["EXPECT_KERNEL"], (rank, geo)
     want = _lib.PATH_PEER if mode not in ("host", "fault") and world <= 4 else _lib.PATH_COLLECTIVE
     # "fault": rank 0's first persistent launch withholds a summary (LPGPU_FAULT);
     # every rank times out in that group, the ranks agree on it and all redo it

@@ -46,3 +46,36 @@ def test_cfg4_shards_sharing_one_gpu(world):
     for p, out in zip(procs, outs):
         assert p.returncode == 0, out[-3000:]
         assert "72 pivots" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m,ns,k,block,tie", [
+    ("mixed", 400, 100, 60, 8, 1e-12),
+    ("mixed", 400, 100, 70, 0, 1e-12),           # auto pivots per sweep
+    ("tall", 900, 40, 50, 32, 1e-12),
+    ("mixed", 48, 32, 40, 4, 0.25),              # wide tie band: straddles across ranks
+])
+def test_one_xcd_cross_rank_selection(kind, m, ns, k, block, tie):
+    """the selection kernel of one rank per GPU (k_sel<XR>: one XCD per rank,
+    the leaving row and pivot row exchanged between ranks) on the one box:
+    two processes forced onto it (LPGPU_XR_XCD=1; small tableaux, so both
+    ranks' blocks are resident on the XCD together), bit-exact"""
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                   WORLD_SIZE="2", LOCAL_RANK="0", LPGPU_XR_XCD="1", LPGPU_STRICT="1", EXPECT_KERNEL="k_sel")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(HERE, "_peer_worker.py"), kind, str(m), str(ns), str(k), str(block),
+             str(tie), "peer"], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
