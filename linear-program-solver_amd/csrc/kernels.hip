@@ -2149,8 +2149,14 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
+        {
+            // write-through stores (SA), as the DPP sweeps'
+            const __amdgpu_buffer_rsrc_t ro = buf_rsrc(Tout + rb * ld + colw);
+            const int voff = (int)(col - colw) * 8, ldb = (int)(ld * 8);
 #pragma unroll
-        for (int k = 0; k < RW; ++k) Tout[(rb + min(k, kmax)) * ld + col] = x[k];
+            for (int k = 0; k < RW; ++k)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, x[k]), ro, voff, min(k, kmax) * ldb, SA);
+        }
     }
     // the group's pivot rows in this run: recomputed after the pass (rare)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2444,23 +2450,31 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
 {
     constexpr int W = 8, RW = 4, SA = 16;
     // LPGPU_SWEEP_DP (A/B): 1 (default) k_sweep_dp2 up to 48 pivots per sweep and
-    // k_sweep_dp at 64 (cfg3 B = 48: 119 against 126-128 us; cfg4 B = 64: 1083-1089
-    // against 1093-1096 us), 2 k_sweep_dp2 always, 3 k_sweep_dp always, 0 k_sweep_st,
-    // 5 k_sweep_rl (pivot rows in registers, rows streamed through LDS)
+    // k_sweep_rl at 64 (round 3: cfg4 906-931 against 978-980 us per launch,
+    // cfg3 at 64 140 against 149 us; at 48 equal, at 32 96 against 93), 2
+    // k_sweep_dp2 always, 3 k_sweep_dp always (round 2's default at 64), 0
+    // k_sweep_st, 5 k_sweep_rl always
     static int dpp = -1;
     if (dpp < 0) {
         const char *v = std::getenv("LPGPU_SWEEP_DP");
         dpp = v ? std::atoi(v) : 1;
     }
-    if (dpp == 5 && A.ld % 64 == 0 && A.ld >= 128) {
-        // k_sweep_rl: 256-column strips, pivot rows in registers, rows and
-        // multipliers streamed into LDS three batches deep
-        constexpr int WL = 4, DL = 3;
+    const int nbq = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
+    if ((dpp == 5 || (dpp == 1 && nbq == 64)) && A.ld % 64 == 0 && A.ld >= 128) {
+        // k_sweep_rl: strips of 64 W columns, pivot rows in registers, rows
+        // and multipliers streamed into LDS one batch ahead (D = 2: measured
+        // faster than 3 deep).  W = 8 waves for long runs (cfg4: 904 against
+        // 930 us at W = 4), 4 for short ones (cfg3: 141 against 149 us)
+        constexpr int DL = 2;
+        const bool w8 = A.rows >= 16384;
         const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
-        const void *fn = nb == 16 ? (const void *)&k_sweep_rl<WL, 16, DL, SA>
-                       : nb == 32 ? (const void *)&k_sweep_rl<WL, 32, DL, SA>
-                       : nb == 48 ? (const void *)&k_sweep_rl<WL, 48, DL, SA>
-                                  : (const void *)&k_sweep_rl<WL, 64, DL, SA>;
+#define RL_FN(WV) (nb == 16 ? (const void *)&k_sweep_rl<WV, 16, DL, SA>   \
+                 : nb == 32 ? (const void *)&k_sweep_rl<WV, 32, DL, SA> \
+                 : nb == 48 ? (const void *)&k_sweep_rl<WV, 48, DL, SA> \
+                            : (const void *)&k_sweep_rl<WV, 64, DL, SA>)
+        const int WL = w8 ? 8 : 4;
+        const void *fn = w8 ? RL_FN(8) : RL_FN(4);
+#undef RL_FN
         const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
         const long long nsg = (A.ld + 64 * WL - 1) / (64 * WL);
         const long long slots = (long long)sweep_cus() * bpc;

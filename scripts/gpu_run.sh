@@ -407,6 +407,21 @@ for step in "$@"; do
             run r3new 900 python -u -m pytest tests/test_gpu_r3.py -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "40000" ;;
         r3procs)
             run r3procs 1000 python -u -m pytest tests/test_gpu_r3_procs.py -v -p no:cacheprovider --timeout 900 --timeout-method thread ${R3P_K:+-k "$R3P_K"} ;;
+        c4ab)
+            # cfg4 on one GPU: default sweep against an LPGPU_SWEEP_DP variant
+            for rep in 1 2; do
+                run c4ab_def_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+                LPGPU_SWEEP_DP=${SWV:-5} run c4ab_sw_$rep 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+            done
+            for f in "$OUT"/c4ab_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 3))"; done ;;
+        c4var)
+            # cfg4 on one GPU, library variants with LPGPU_SWEEP_DP=${SWV:-5}
+            for V in ${C4_VARIANTS:-main}; do
+                L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants/$V.so
+                [ "$V" = main ] && L=$PWD/linear-program-solver_amd/lpsol_amd/_lib/liblpgpu.so
+                LPGPU_LIB=$L LPGPU_SWEEP_DP=${SWV:-5} run c4var_$V 300 python bench.py --no-cpu-baseline --no-cfg3 --steps 24 --warmup 4
+            done
+            for f in "$OUT"/c4var_*.log; do python3 -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'], 1), 'frac', round(d['roofline']['frac'], 3), 'sel', round(d['selection']['us_per_pivot'], 3))"; done ;;
         r3f)
             run r3f 300 python -u -m pytest tests/test_gpu_r2.py -k timeout -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         clk)
