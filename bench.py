@@ -47,9 +47,9 @@ from lpsol_amd import generators as gen  # noqa: E402
 METRIC = "pivots/sec + achieved HBM GB/s on dense float64 tableau, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F64_PEAK_TFLOPS = 78.6      # float64 vector spec (half the guide's 157.3 TF FP32 vector)
-SWEEP_KERNEL = "k_sweep_dp"
+SWEEP_KERNEL = "k_sweep"          # every sweep kernel's name starts so (the traffic stamp names which)
 SEED = 3
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r02", "hbm_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "hbm_traffic.json")
 
 # name -> (generator kind, m, ns, description)
 WORKLOADS = {
@@ -103,8 +103,8 @@ def src_digest() -> str:
 
 def sweep_kernel(block: int) -> str:
     """the sweep kernel the engine launches for `block` pivots per sweep
-    (kernels.hip launch_sweep: k_sweep_dp2 up to 48, k_sweep_dp at 64)"""
-    return "k_sweep_dp2" if block <= 48 else "k_sweep_dp"
+    (kernels.hip launch_sweep: k_sweep_dp2 up to 48, k_sweep_rl at 64)"""
+    return "k_sweep_dp2" if block <= 48 else "k_sweep_rl"
 
 
 def load_traffic(path: str | None, block: int, workload_name: str, digest: str):

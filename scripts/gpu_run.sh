@@ -221,10 +221,9 @@ for step in "$@"; do
             for W in ${PMC_WORKLOADS:-cfg4 cfg3}; do
                 run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
                 run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
-                PB=$([ "$W" = cfg4 ] && echo 64 || echo 48)   # the engine's auto pivots per sweep
-                run pmc_json_$W 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch_$W" "$OUT/pmc_write_$W" profiles/r02/hbm_traffic.json --block $PB --kernel k_sweep_dp --workload $W
-            done
-            cp profiles/r02/hbm_traffic.json "$OUT/hbm_traffic.json" ;;
+                PB=64   # the engine's auto pivots per sweep (cfg4 and, since round 3, cfg3)
+                run pmc_json_$W 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch_$W" "$OUT/pmc_write_$W" "$OUT/hbm_traffic.json" --block $PB --kernel k_sweep_rl --workload $W
+            done ;;
         proffinal)
             export TMPDIR=/tmp
             run rocprof_final 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_final" -o run -- python3 "$PWD/bench.py" --no-cpu-baseline ;;
