@@ -158,7 +158,7 @@ struct Args {
     // tagged granules -- ratio, row 0, XCD check, and the fourth: k_group's
     // two-level exchange (8 ratio + 8 row-0 level-2 slots) / k_sel's rescan
     // and owner answers
-    unsigned long long *gran;
+    unsigned long long *gran;   // GRAN_TOTAL granules (below)
     unsigned spin_max;   // k_group: polls of one exchange before it gives up (timeout)
     unsigned xwait_ms;   // k_group (XR): wall-clock bound of a cross-rank wait
     int fault;           // tests only (LPGPU_FAULT): t + 1 -> block 1 withholds pivot t's ratio summary
@@ -201,6 +201,13 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
 
 constexpr int GROUP_MAXBLOCKS = 256;
 constexpr int GRAN_REGIONS = 4;       // regions of Args::gran (see there)
+// Args::gran: one set of GRAN_REGIONS regions of GROUP_MAXBLOCKS x 8 granules
+// per XCD shard of the XCD-sharded selection (k_sel<XS>, select.hip; every
+// other persistent selection uses set 0), then the shards' common region
+// (their leaving-row summaries and straddle answers)
+constexpr int XS_SHARDS = 8;          // XCD shards of one device (MI355X: 8 XCDs)
+constexpr long long GRAN_SHARD = (long long)GRAN_REGIONS * GROUP_MAXBLOCKS * 8;
+constexpr long long GRAN_TOTAL = (XS_SHARDS + 1) * GRAN_SHARD;
 constexpr int GROUP_MINBLOCKS = 64;    // a small tableau still spreads its columns over 64 blocks
 constexpr int GROUP_THREADS = 64;      // one wave: block reductions stay in registers
 constexpr int GROUP_MAXRPL = 4;        // own rows per lane (<= 64 x 256 x 4 = 65536 rows per device, as LDS allows)
@@ -227,15 +234,21 @@ struct GroupGeom {
     size_t lds = 0;      // dynamic LDS per block
     int per_cu = 0;      // resident blocks per CU the launch relies on
     int sel = 0;         // > 0: the one-XCD selection k_sel (select.hip) for up to `sel` pivots per launch
+    int xs = 0;          // > 0: k_sel split into `xs` row shards, one per XCD, in one launch (g blocks each)
 };
 // rc: local constraint rows (the largest shard's for a sharded job); bmax:
 // pivots per group; xr: 0 single device, 1 row-sharded rank, 2 row-sharded
 // rank that may use one XCD; nshard: in-process shards in one launch; share:
-// processes whose launches must be resident on this device at the same time.
-GroupGeom group_geom(long long rc, long long ld, long long n, int bmax, int xr, int nshard, int share);
+// processes whose launches must be resident on this device at the same time;
+// xs_ok: a single-device tableau too tall for one XCD may take k_sel's XCD
+// shards (else k_group).
+GroupGeom group_geom(long long rc, long long ld, long long n, int bmax, int xr, int nshard, int share,
+                     bool xs_ok = true);
 // the one-XCD selection (select.hip): g <= 64 blocks, one own row per lane,
-// the variable columns 1..n split evenly; g == 0 if the shape does not fit
-GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr);
+// the variable columns 1..n split evenly; g == 0 if the shape does not fit.
+// xs_ok (single device): a tableau too tall for one XCD may run as XS_SHARDS
+// row shards of <= 64 g rows, one per XCD, in one launch (geo.xs)
+GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok);
 hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int grp, int count, int from_erec,
                       unsigned seq, int xr, int first, int fmode, int frule, long long fcap, hipEvent_t e0,
                       hipEvent_t e1);

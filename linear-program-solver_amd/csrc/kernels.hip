@@ -2620,7 +2620,7 @@ static int group_per_cu(const void *fn, size_t lds)
 }
 
 static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, int bmax, int xr, int nshard,
-                                     int share)
+                                     int share, bool xs_ok)
 {
     GroupGeom G;
     if (rc < 1 || ld < 1 || ld >= 0x7fffffffLL || rc >= 0x7fffffffLL || bmax < 1 || bmax > BMAX ||
@@ -2633,7 +2633,7 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, in
     }
     // the one-XCD selection k_sel (select.hip) where the shape fits it
     if (xcd_on && xr != 1 && nshard == 1 && share == 1) {
-        const GroupGeom S = sel_geom(rc, n, bmax, sweep_cus() / 8, xr != 0);
+        const GroupGeom S = sel_geom(rc, n, bmax, sweep_cus() / 8, xr != 0, xs_ok && xr == 0);
         if (S.g > 0) return S;
     }
     static long long gmin_env = -1;
@@ -2725,17 +2725,17 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, in
     return GroupGeom{};
 }
 
-GroupGeom group_geom(long long rc, long long ld, long long n, int bmax, int xr, int nshard, int share)
+GroupGeom group_geom(long long rc, long long ld, long long n, int bmax, int xr, int nshard, int share, bool xs_ok)
 {
     static std::mutex mu;
-    static std::map<std::array<long long, 8>, GroupGeom> cache;
+    static std::map<std::array<long long, 9>, GroupGeom> cache;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const std::array<long long, 8> key{rc, ld, n, bmax, xr, nshard, share, dev};
+    const std::array<long long, 9> key{rc, ld, n, bmax, xr, nshard, share, dev, xs_ok ? 1 : 0};
     std::lock_guard<std::mutex> lk(mu);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
-    const GroupGeom G = group_geom_uncached(rc, ld, n, bmax, xr, nshard, share);
+    const GroupGeom G = group_geom_uncached(rc, ld, n, bmax, xr, nshard, share, xs_ok);
     cache[key] = G;
     return G;
 }

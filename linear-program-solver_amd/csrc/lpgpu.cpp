@@ -53,6 +53,8 @@ struct lp_handle {
     unsigned xwait_ms = 30000;      // bound of a cross-rank wait (XR)
     int fault_launch = 0, fault_t = 0;   // tests: LPGPU_FAULT=<launch>:<pivot>
     bool strict = false;            // LPGPU_STRICT=1 (tests): a timed-out group is an error
+    bool xs_ok = true;              // a tall single-device tableau may take k_sel's XCD shards
+                                    // (LPGPU_SEL_XS=0 / lpdiag_set_xcd_shards: k_group instead)
     // row-sharded persistent selection: device-side exchange between ranks
     unsigned long long *xbuf = nullptr;     // this rank's exchange buffer (peers write it)
     unsigned long long **dpeer = nullptr;   // device table: every rank's buffer
@@ -390,6 +392,7 @@ static int alloc_handle(lp_handle *h)
     if (const char *v = std::getenv("LPGPU_XWAIT_MS")) h->xwait_ms = (unsigned)std::strtoul(v, nullptr, 10);
     if (const char *v = std::getenv("LPGPU_FAULT")) std::sscanf(v, "%d:%d", &h->fault_launch, &h->fault_t);
     if (const char *v = std::getenv("LPGPU_STRICT")) h->strict = v[0] == '1';
+    if (const char *v = std::getenv("LPGPU_SEL_XS")) h->xs_ok = v[0] != '0';
     if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
     if (const char *st = std::getenv("LPGPU_STAMPS"))
         if (st[0] == '1') {
@@ -411,7 +414,7 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMemsetAsync(h->MQ, 0, mqbytes, h->s));
     HCHK(h, hipMalloc(&h->M, mbytes));
     HCHK(h, hipMemsetAsync(h->M, 0, mbytes, h->s));
-    const size_t gbytes = lpk::GRAN_REGIONS * lpk::GROUP_MAXBLOCKS * 8 * sizeof(unsigned long long);
+    const size_t gbytes = (size_t)lpk::GRAN_TOTAL * sizeof(unsigned long long);
     HCHK(h, hipMalloc(&h->gran, gbytes));
     HCHK(h, hipMemsetAsync(h->gran, 0, gbytes, h->s));
     HCHK(h, hipMalloc(&h->row0, (size_t)h->ld * sizeof(double)));
@@ -929,7 +932,7 @@ static lpk::GroupGeom persistent_geom_b(lp_handle *h, size_t nmem, int *xr, int 
     *xr = 0;
     lpk::GroupGeom none;
     if (!h->persistent) return none;
-    if (!h->comm) return lpk::group_geom(h->rc, h->ld, h->n, bmax, 0, 1, 1);
+    if (!h->comm) return lpk::group_geom(h->rc, h->ld, h->n, bmax, 0, 1, 1, h->xs_ok);
     if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
     *xr = (nmem == 1 && h->xr_xcd) ? 2 : 1;
@@ -1691,8 +1694,9 @@ extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
 // own columns per lane, own rows per lane, summaries per lane, one-XCD grid,
 // k_group's two-level variant, k_sel's pivot capacity (0: k_group),
 // Ctl::sel_flags of the last launch (1 one XCD, 2 two-level exchange engaged,
-// 4 k_sel, 8 k_sel's blocks were not on one XCD); all 0 when the per-pivot
-// kernels run
+// 4 k_sel, 8 k_sel's blocks were not on one XCD, 16 k_sel as XCD shards), the
+// XCD shards of the launch (out[8], 0: none); all 0 when the per-pivot kernels
+// run
 extern "C" int lpdiag_geometry(lp_handle *h, long long *out)
 {
     const Members M = members_of(h);
@@ -1706,6 +1710,18 @@ extern "C" int lpdiag_geometry(lp_handle *h, long long *out)
     out[5] = g.hk;
     out[6] = g.sel;
     out[7] = h->hctl->sel_flags;
+    out[8] = g.xs;
+    return LP_PIVOTED;
+}
+
+// diagnostics / A/B: whether a tall single-device tableau may run k_sel as XCD
+// shards (1, default) or takes k_group (0); re-chooses the automatic pivots per
+// sweep
+extern "C" int lpdiag_set_xcd_shards(lp_handle *h, int on)
+{
+    if (!h) return LP_BAD_ARG;
+    h->xs_ok = on != 0;
+    h->block_auto = 0;
     return LP_PIVOTED;
 }
 

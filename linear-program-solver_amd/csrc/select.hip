@@ -39,6 +39,7 @@
 #include <hip/hip_ext.h>
 
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -70,7 +71,7 @@ namespace {
 // 5 every row-0 summary seen
 #define SEL_EV(k)                                                                                   \
     do {                                                                                            \
-        if (A.stamps && lane == 0 && t < 48)                                                        \
+        if (A.stamps && lane == 0 && t < 48 && shard == 0)                                          \
             *gp(A.stamps + BMAX * 16 + 4096 + ((long long)t * 64 + b) * 8 + (k)) =                  \
                 (long long)__builtin_amdgcn_s_memrealtime();                                        \
     } while (0)
@@ -329,7 +330,8 @@ __device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, u
 // every block's summary (lane l: block min(l, G - 1)); polls until every
 // granule carries `tag`, bounded by spin_max polls (the host then redoes the
 // group on the per-pivot kernels)
-template <int NG>
+// (STRIDE: granules between granule g and g + 1 of a slot)
+template <int NG, int STRIDE = SEL_SLOT>
 __device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (&w)[NG], unsigned *timeout_flag,
                            unsigned spin_max)
 {
@@ -338,7 +340,7 @@ __device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (
         bool ok = true;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
-            const u64 v = ld_sc1(p + g * SEL_SLOT);
+            const u64 v = ld_sc1(p + g * STRIDE);
             w[g] = (unsigned)v;
             ok = ok && (unsigned)(v >> 32) == tag;
         }
@@ -475,7 +477,7 @@ constexpr int SEL_NGX = 7;   // XR rank summary: l (2), global row, a (2), b (2)
         m1[u_] = kq_ == 1 ? apend : m1[u_];                                                         \
         if constexpr (NK > 2) m2[u_] = kq_ == 2 ? apend : m2[u_];                                   \
         if constexpr (NK > 3) m3[u_] = kq_ == 3 ? apend : m3[u_];                                   \
-        if (own) stx<FAST>(at(Mb + (long long)tq_ * rowsv, moff), apend);                           \
+        if (own) stx<FAST && !XS>(at(Mb + (long long)tq_ * rowsv, moff), apend);                    \
         if (zpend) {                                                                                \
             m0 = (d16)0.0;                                                                          \
             if (tq_ >= 16) m1 = (d16)0.0;                                                           \
@@ -488,12 +490,20 @@ constexpr int SEL_NGX = 7;   // XR rank summary: l (2), global row, a (2), b (2)
 // multipliers); IPL: own columns per lane (cpb <= 64 IPL); XR: one rank of a
 // row-sharded job (leaving row and pivot row exchanged between ranks through
 // the peers' exchange buffers, as in k_group); FAST: every block on one XCD.
+// XS: shard `shard` of XS_SHARDS row shards of ONE tableau, one per XCD, in
+// one launch: the shard's G blocks own rows [1 + shard rps, 1 + shard rps +
+// rps) and, like every shard, all the variable columns; the shards exchange
+// their leaving-row candidates through the common region of Args::gran, and
+// every shard forms the winner's pivot row itself from the shared tableau (the
+// multipliers are stored write-through for that) -- no row travels.
 // first: as k_group's (call start: reset / eager / enter).
-template <int IPL, int NB, bool XR, bool FAST>
+template <int IPL, int NB, bool XR, bool FAST, bool XS>
 __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const unsigned G, int grp, int count,
                                          int from_erec, unsigned seq, int first, int fmode, long long fcap,
-                                         double *lP, long long npiv, long long nstd, long long stuck, int rule)
+                                         double *lP, long long npiv, long long nstd, long long stuck, int rule,
+                                         const unsigned shard)
 {
+    static_assert(!(XR && XS), "k_sel: XS is one device");
     constexpr int CS = NB + 2;             // LDS stride of a column's pivot values (16-B reads, no conflicts)
     constexpr int NK = NB / 16;            // broadcast registers
     const int lane = threadIdx.x;
@@ -522,8 +532,11 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     tol.stall = vgpr(A.tol.stall);
     // own rows: lane l holds row lr0 + l; own columns: j = jc0 + l + 64 k, a
     // block's share of the variable columns 1..n (column 0 is every block's)
-    const long long rpb = (A.rc + G - 1) / G;
-    const long long lr0 = vgpr(1 + (long long)b * rpb), lr1 = vgpr(min(1 + (long long)b * rpb + rpb, A.rows));
+    const long long rps = XS ? (A.rc + XS_SHARDS - 1) / XS_SHARDS : A.rc;   // rows of a shard
+    const long long rs0 = XS ? (long long)shard * rps : 0;                   // its first (0-based)
+    const long long rpb = (rps + G - 1) / G;
+    const long long lr0 = vgpr(1 + rs0 + (long long)b * rpb),
+                    lr1 = vgpr(min(1 + rs0 + min((long long)b * rpb + rpb, rps), A.rows));
     const long long li = lr0 + lane;
     const bool own = li < lr1;
     const long long cpb = (A.n + G - 1) / G;
@@ -569,10 +582,13 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     // LDS pivot values start at zero: the chains' padding pivots multiply them by 0
     for (long long e = lane; e < (cpb * CS + 8) / 2; e += GROUP_THREADS)
         reinterpret_cast<double2 *>(lP)[e] = make_double2(0.0, 0.0);
-    // summary regions: ratio, row 0, XCD check, rescan answers
-    u64 *const grR = vgpr(A.gran);
-    u64 *const grE = vgpr(A.gran + GROUP_MAXBLOCKS * GSLOT);
-    u64 *const grS = vgpr(A.gran + 3 * GROUP_MAXBLOCKS * GSLOT);
+    // summary regions: ratio, row 0, XCD check, rescan answers (XS: the
+    // shard's own set; xsum: the shards' common region)
+    u64 *const gset = A.gran + (XS ? (long long)shard * GRAN_SHARD : 0);
+    u64 *const grR = vgpr(gset);
+    u64 *const grE = vgpr(gset + GROUP_MAXBLOCKS * GSLOT);
+    u64 *const grS = vgpr(gset + 3 * GROUP_MAXBLOCKS * GSLOT);
+    u64 *const xsum = vgpr(A.gran + XS_SHARDS * GRAN_SHARD);
     ERec *const erecv = vgpr(A.erec);
     long long *const logv = vgpr(A.log);
     long long *const dRv = vgpr(A.dR);
@@ -747,7 +763,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         // summary (read from pivot t + 1 on); this pivot's multipliers are
         // stored after it and drained with the next one
         drain_stores();
-        if (!(A.fault == t + 1 && b == min(1u, G - 1))) {   // fault injection (tests): block 1 (0) never publishes
+        if (!(A.fault == t + 1 && b == min(1u, G - 1) && shard == 0)) {   // fault injection (tests): block 1 (0) never publishes
             unsigned wv = idx32(ib);
             wv = wl(wv, lo32(lb), 0);
             wv = wl(wv, hi32(lb), 1);
@@ -813,7 +829,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 aR = rl_d(y[1], y[2], 0);
                 bR = rl_d(y[3], y[4], 0);
             }
-        } else if (!XR) {
+        } else if (!XR && !XS) {
             status = LP_UNBOUNDED;
             break;
         }
@@ -1002,6 +1018,95 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             }
             xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
             p0 = bR / aR;
+        } else if constexpr (XS) {
+            // ---- leaving row across the XCD shards: block 0 of every shard
+            //      publishes (shard minimum, row, pivot element, b), write-
+            //      through, granule-major (one poll instruction reads granule
+            //      g of all shards: 64 bytes); every block takes the first
+            //      shard inside the global band (rows are shard-ordered, so
+            //      that is the reference's first row)
+            const int par = t & 1;
+            u64 *const xsl = xsum + par * 128;
+            if (b == 0 && lane < SEL_NGX) {
+                unsigned wv = R == NONE ? 0xffffffffu : (unsigned)(R - 1);
+                wv = wl(wv, lo32(g), 0);
+                wv = wl(wv, hi32(g), 1);
+                wv = wl(wv, lo32(aR), 3);
+                wv = wl(wv, hi32(aR), 4);
+                wv = wl(wv, lo32(bR), 5);
+                wv = wl(wv, hi32(bR), 6);
+                st_sc1(&xsl[lane * XS_SHARDS + shard], ((u64)gtag(seq, t, 2) << 32) | wv);
+            }
+            unsigned x[SEL_NGX];
+            const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
+            if (!sel_gather<SEL_NGX, XS_SHARDS>(xsl, XS_SHARDS, gtag(seq, t, 2), x, &ctlv->bar_timeout, spin)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
+            const double lp = lane < XS_SHARDS ? mk_d(x[0], x[1]) : INFINITY;
+            const double gg = wmin(lp);
+            if (!(gg < INFINITY)) {
+                status = LP_UNBOUNDED;
+                break;
+            }
+            const double thr = tie_band(gg, tol.ratio_tie);
+            const int ps = __builtin_ctzll(__ballot(lane < XS_SHARDS && lp <= thr));
+            double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
+            bool okp;
+            const double qs = row_ratio(as, bs, tol, okp);
+            long long rg;
+            if (okp && qs <= thr) {
+                rg = (long long)rl32(x[2], ps);
+            } else {
+                // rare: a near-tie straddles the band across shards.  Shard
+                // ps's blocks each offer their first own row inside it (its
+                // rescan slots), its block 0 publishes the lowest to all
+                u64 *const xst = xsum + 256 + par * 8;
+                if ((int)shard == ps) {
+                    const u64 mk = __ballot(okq && q <= thr);
+                    const int fr = mk ? __builtin_ctzll(mk) : 0;
+                    const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
+                    u64 *const loc = grS + 1024;
+                    if (lane < SEL_NGS) {
+                        unsigned wv = mk ? (unsigned)(lr0 + fr) : 0x7fffffffu;
+                        wv = wl(wv, lo32(ar), 1);
+                        wv = wl(wv, hi32(ar), 2);
+                        wv = wl(wv, lo32(br), 3);
+                        wv = wl(wv, hi32(br), 4);
+                        st_sc1(&loc[b * 8 + lane], ((u64)gtag(seq, t, 4) << 32) | wv);
+                    }
+                    unsigned wlo[1][SEL_NGS];
+                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wlo, &ctlv->bar_timeout, spin)) {
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
+                    if (b == 0 && lane < SEL_NGS) {
+                        unsigned wv = rl32(wlo[0][0], bf) - 1u;
+                        wv = wl(wv, rl32(wlo[0][1], bf), 1);
+                        wv = wl(wv, rl32(wlo[0][2], bf), 2);
+                        wv = wl(wv, rl32(wlo[0][3], bf), 3);
+                        wv = wl(wv, rl32(wlo[0][4], bf), 4);
+                        st_sc1(&xst[lane], ((u64)gtag(seq, t, 5) << 32) | wv);
+                    }
+                }
+                unsigned y[SEL_NGS];
+                if (!sel_gather<SEL_NGS, 1>(xst, 1, gtag(seq, t, 5), y, &ctlv->bar_timeout, spin)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                rg = (long long)__builtin_amdgcn_readfirstlane(y[0]);
+                as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
+                bs = mk_d(__builtin_amdgcn_readfirstlane(y[3]), __builtin_amdgcn_readfirstlane(y[4]));
+            }
+            rglob = rg;
+            R = rg + 1;
+            aR = as;
+            bR = bs;
+            xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
+            // every shard: the pivot row on its blocks' columns from the
+            // stored row and the leaving row's multipliers (write-through)
+            prow(R, aR);
         } else {
             prow(R, aR);
         }
@@ -1179,7 +1284,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         SEL_CLK(0);
     }
 #ifdef LPK_STAMPS
-    if (A.stamps && lane == 0) {
+    if (A.stamps && lane == 0 && shard == 0) {
         long long *o = A.stamps + BMAX * 16 + (long long)b * 32;
         for (int k = 0; k < 16; ++k) o[k] = (long long)clk_[k];
         o[16] = ndone;
@@ -1208,7 +1313,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             *gp(&col0v[0]) = v0;
         }
     }
-    if (XR && b == 0 && lane == 0) {
+    if ((XR || XS) && b == 0 && lane == 0 && shard == 0) {
         *gp(&ctl->xwait_ticks) += xwait;
         *gp(&ctl->xwait_pivots) += ndone;
     }
@@ -1221,21 +1326,24 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
 
 }  // namespace
 
-template <int IPL, int NB, bool XR>
+template <int IPL, int NB, bool XR, bool XS>
 __global__ void __launch_bounds__(GROUP_THREADS)
 k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int first, int fmode, int frule,
       long long fcap)
 {
     static_assert(NB % 16 == 0 && NB <= BMAX, "k_sel: pivots per launch");
-    // the grid is 8 x G and only blocks 0, 8, 16, ... work: they share one XCD
-    // under the round-robin dealing of workgroups (checked below)
-    if (blockIdx.x & 7u) return;
+    // the grid is 8 x G.  One XCD: only blocks 0, 8, 16, ... work -- they share
+    // one XCD under the round-robin dealing of workgroups (checked below).
+    // XS: every block works, block 8 b + x being block b of shard x (so each
+    // shard's blocks share one XCD, checked below, and each XCD holds one shard)
+    if (!XS && (blockIdx.x & 7u)) return;
     extern __shared__ __attribute__((aligned(16))) double lP[];   // [cpb][NB + 2]: P[s][own column]
     const unsigned b = blockIdx.x >> 3, G = (unsigned)gper;
+    const unsigned shard = XS ? (blockIdx.x & 7u) : 0u;
     const int lane = threadIdx.x;
     Ctl *const ctl = A.ctl;
     const bool reset = (first & 1) != 0;
-    if (b == 0 && lane == 0) *gp(&ctl->ndef[grp]) = 0;
+    if (b == 0 && lane == 0 && shard == 0) *gp(&ctl->ndef[grp]) = 0;
     if (!reset && (ld_sc1(&ctl->status) != LP_PIVOTED || ld_sc1(&ctl->bar_timeout) != 0u)) return;
     long long npiv = reset ? 0 : ld_sc1(&ctl->npiv);
     int rule = reset ? frule : ld_sc1(&ctl->rule);
@@ -1245,7 +1353,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         stuck = ld_sc1(&ctl->stuck);
     }
     rule = __builtin_amdgcn_readfirstlane(rule);
-    if (lane == 0) {
+    if (lane == 0 && shard == 0) {
         // the loop state before this group: what a timed-out group is redone from
         st_sc1(&ctl->g_npiv, npiv);
         st_sc1(&ctl->g_nstd, nstd);
@@ -1255,14 +1363,15 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     }
     {
         // every block publishes its XCD.  The hand-offs are plain stores that
-        // stay in the XCD's L2, correct only if every block runs there: if not
-        // (never seen), the group is abandoned like a timed-out one and the
-        // host redoes it on the per-pivot kernels (lpgpu.cpp recover_timeout).
-        // (The eager row-0 copies of a call's first launch are drained by its
-        // entering-column exchange, not by this one.)
+        // stay in the XCD's L2, correct only if every block (of the shard)
+        // runs there: if not (never seen), the group is abandoned like a
+        // timed-out one and the host redoes it on the per-pivot kernels
+        // (lpgpu.cpp recover_timeout).  (The eager row-0 copies of a call's
+        // first launch are drained by its entering-column exchange, not by
+        // this one.)
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-        u64 *const grX = A.gran + 2 * GROUP_MAXBLOCKS * GSLOT;
+        u64 *const grX = A.gran + (XS ? (long long)shard * GRAN_SHARD : 0) + 2 * GROUP_MAXBLOCKS * GSLOT;
         drain_stores();
         if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | xcc);
         unsigned wx[1];
@@ -1279,20 +1388,24 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             return;
         }
     }
-    if (b == 0 && lane == 0) *gp(&ctl->sel_flags) = 1u | 4u;   // diagnostics
-    sel_body<IPL, NB, XR, true>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
-                                rule);
+    // diagnostics: 1 one XCD, 4 k_sel, 16 XCD shards
+    if (b == 0 && lane == 0 && shard == 0) *gp(&ctl->sel_flags) = XS ? (16u | 4u) : (1u | 4u);
+    sel_body<IPL, NB, XR, true, XS>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
+                                    rule, shard);
 }
 
 // ---- geometry and launch ----------------------------------------------------
 namespace {
 
-const void *sel_kernel(int ipl, int nb, bool xr)
+const void *sel_kernel(int ipl, int nb, bool xr, bool xs)
 {
-#define SEL_K(I, N) (xr ? reinterpret_cast<const void *>(&k_sel<I, N, true>) \
-                        : reinterpret_cast<const void *>(&k_sel<I, N, false>))
+#define SEL_K(I, N) (xr ? reinterpret_cast<const void *>(&k_sel<I, N, true, false>) \
+                        : reinterpret_cast<const void *>(&k_sel<I, N, false, false>))
+#define SEL_XS(I) reinterpret_cast<const void *>(&k_sel<I, 64, false, true>)
+    if (xs) return nb != 64 || xr ? nullptr : ipl == 1 ? SEL_XS(1) : ipl == 2 ? SEL_XS(2) : SEL_XS(4);
     if (nb == 32) return ipl == 1 ? SEL_K(1, 32) : ipl == 2 ? SEL_K(2, 32) : SEL_K(4, 32);
     return ipl == 1 ? SEL_K(1, 64) : ipl == 2 ? SEL_K(2, 64) : SEL_K(4, 64);
+#undef SEL_XS
 #undef SEL_K
 }
 
@@ -1314,7 +1427,7 @@ int sel_per_cu(const void *fn, size_t lds)
 
 }  // namespace
 
-GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr)
+GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok)
 {
     GroupGeom G;
     static int on = -1;
@@ -1323,24 +1436,48 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr)
         on = v ? std::atoi(v) : 1;
     }
     if (!on || rc < 1 || n < 1 || bmax < 1 || bmax > BMAX) return G;
-    const long long grows = (rc + 63) / 64;
-    long long g = std::max(grows, (n + 255) / 256);
-    if (g > 64) return G;
-    const long long cpb = (n + g - 1) / g;
-    int ipl = (int)((cpb + 63) / 64);
-    if (ipl == 3) ipl = 4;
-    if (ipl > 4) return G;
+    // one XCD, or (too tall for one: more than 64 x 64 rows) XS_SHARDS row
+    // shards of rps rows, one per XCD, each shard's blocks over all columns
+    int xs = 0;
+    long long rps = rc;
+    if ((rc + 63) / 64 > 64) {
+        if (!xs_ok || xr || bmax <= 32) return G;
+        xs = XS_SHARDS;
+        rps = (rc + XS_SHARDS - 1) / XS_SHARDS;
+    }
+    // the fewest blocks (g) with every lane at most 4 columns, or more where
+    // a block's LDS (the pivot values of its columns) leaves too few blocks
+    // per CU for g on one XCD
+    const long long g0 = std::max((rps + 63) / 64, (n + 255) / 256);
     const int nb = bmax <= 32 ? 32 : 64;
-    const size_t lds = ((size_t)cpb * (nb + 2) + 8) * sizeof(double);   // + the row chain's read-ahead slack
-    const void *fn = sel_kernel(ipl, nb, xr);
-    const int per_cu = sel_per_cu(fn, lds);
-    if (per_cu < 1 || g > (long long)per_cu * xcd_cus) return G;
+    long long g = 0, cpb = 0;
+    int ipl = 0, per_cu = 0;
+    size_t lds = 0;
+    for (long long gc = g0; gc <= 64; gc = gc < 64 && gc + 8 > 64 ? 64 : gc + 8) {
+        cpb = (n + gc - 1) / gc;
+        ipl = (int)((cpb + 63) / 64);
+        if (ipl == 3) ipl = 4;
+        if (ipl > 4) continue;
+        lds = ((size_t)cpb * (nb + 2) + 8) * sizeof(double);   // + the row chain's read-ahead slack
+        const void *fn = sel_kernel(ipl, nb, xr, xs > 0);
+        if (!fn) return G;
+        per_cu = sel_per_cu(fn, lds);
+        if (std::getenv("LPGPU_GEOM_DEBUG"))
+            fprintf(stderr, "sel_geom rc %lld n %lld bmax %d xs %d g %lld ipl %d lds %zu per_cu %d xcd_cus %d\n", rc,
+                    n, bmax, xs, gc, ipl, lds, per_cu, xcd_cus);
+        if (per_cu >= 1 && gc <= (long long)per_cu * xcd_cus) {
+            g = gc;
+            break;
+        }
+    }
+    if (g == 0) return G;
     G.g = g;
     G.nr = 1;
     G.ipl = ipl;
     G.rpl = 1;
     G.xmode = 1;
     G.sel = nb;
+    G.xs = xs;
     G.lds = lds;
     G.per_cu = per_cu;
     return G;
@@ -1352,8 +1489,10 @@ hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int gr
 {
     if (geo.g == 0 || geo.sel == 0 || count < 1 || count > geo.sel) return hipErrorInvalidValue;
     if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
-    if (A.rc > 64 * geo.g || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
-    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0);
+    if (geo.xs && (geo.xs != XS_SHARDS || xr)) return hipErrorInvalidValue;
+    if (A.rc > 64 * geo.g * (geo.xs ? XS_SHARDS : 1) || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
+    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0, geo.xs > 0);
+    if (!fn) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(geo.g * 8));
     Args a0 = A;
     int gper = (int)geo.g;

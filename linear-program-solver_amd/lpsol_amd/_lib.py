@@ -322,14 +322,20 @@ class Engine:
     def geometry(self) -> dict:
         """diagnostics (lpdiag_geometry): the persistent selection's launch
         geometry for this handle and what its last launch found on the device"""
-        out = (C.c_longlong * 8)()
+        out = (C.c_longlong * 9)()
         self._check(self.lib.lpdiag_geometry(self.h, out), self.h)
-        keys = ("blocks", "ipl", "rpl", "nr", "one_xcd_grid", "two_level_variant", "sel", "flags")
+        keys = ("blocks", "ipl", "rpl", "nr", "one_xcd_grid", "two_level_variant", "sel", "flags", "xcd_shards")
         d = dict(zip(keys, list(out)))
         d["kernel"] = "none" if d["blocks"] == 0 else "k_sel" if d["sel"] else "k_group"
         d["on_one_xcd"] = bool(d["flags"] & 1)
         d["two_level_engaged"] = bool(d["flags"] & 2)
+        d["xcd_shards_engaged"] = bool(d["flags"] & 16)
         return d
+
+    def set_xcd_shards(self, on: bool):
+        """diagnostics / A/B (lpdiag_set_xcd_shards): a tall single-device
+        tableau runs k_sel as one row shard per XCD (default) or k_group"""
+        self._check(self.lib.lpdiag_set_xcd_shards(self.h, 1 if on else 0), self.h)
 
     def get_block(self) -> int:
         """pivots per sweep in use (the auto choice resolved)"""

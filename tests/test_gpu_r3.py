@@ -35,10 +35,12 @@ def gpu():
     assert _lib.device_count() > 0, "no GPU visible"
 
 
-def _engine(T, block=0):
+def _engine(T, block=0, xcd_shards=True):
     e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
     e.upload(T)
     e.set_block(block)
+    if not xcd_shards:
+        e.set_xcd_shards(False)
     return e
 
 
@@ -95,18 +97,22 @@ def cfg4_136():
     return T, o.T, olog
 
 
-def test_cfg4_timed_configuration(cfg4_136):
+@pytest.mark.parametrize("xcd_shards", [True, False])
+def test_cfg4_timed_configuration(cfg4_136, xcd_shards):
     """cfg4 on one GPU as the bench runs it: 64 pivots per sweep (auto),
-    the spread persistent selection with the two-level exchange, 136 pivots,
-    no fallback, bit-exact"""
+    the persistent selection as 8 XCD shards of k_sel (the default) or
+    k_group's two-level exchange, 136 pivots, no fallback, bit-exact"""
     T, want, olog = cfg4_136
-    e = _engine(T)
+    e = _engine(T, 0, xcd_shards)
     st, done = e.run(_lib.RULE_STANDARD, 136)
     assert st == _lib.PIVOTED and done == 136
     assert e.get_block() == 64
     assert e.exchange_path() == (_lib.PATH_PERSISTENT, 0)
     geo = e.geometry()
-    assert geo["kernel"] == "k_group" and geo["two_level_engaged"], geo
+    if xcd_shards:
+        assert geo["kernel"] == "k_sel" and geo["xcd_shards"] == 8 and geo["xcd_shards_engaged"], geo
+    else:
+        assert geo["kernel"] == "k_group" and geo["two_level_engaged"], geo
     assert e.log().tolist() == olog.tolist()
     assert np.array_equal(e.download(), want)
     e.close()
@@ -161,7 +167,7 @@ def test_two_level_timeout_recovery(monkeypatch):
     monkeypatch.setenv("LPGPU_SPIN_MAX", "20000")
     monkeypatch.delenv("LPGPU_STRICT", raising=False)
     T = gen.tableau(*TALL)
-    e = _engine(T, 64)
+    e = _engine(T, 64, False)
     st, done = e.run(_lib.RULE_STANDARD, 40)
     o = F64Tableau(T)
     ost, olog = o.run(0, 40)
@@ -179,7 +185,7 @@ def test_two_level_objective_increased():
     o0 = F64Tableau(T)
     r, c = o0.find(0)
     T[1 + r, 0] = -1.0 / 64           # the row the ratio test picks first
-    e = _engine(T, 64)
+    e = _engine(T, 64, False)
     st, npiv, nstd = e.solve()
     o = F64Tableau(T)
     ost, olog, onstd = o.solve()

@@ -79,6 +79,7 @@ def test_spread_selection_two_level_exchange(rule, tie):
     e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
     e.upload(T)
     e.set_block(64)
+    e.set_xcd_shards(False)            # k_group (the XCD-sharded k_sel: test_gpu_xs.py)
     e.set_tol(cost_tie=tie, ratio_tie=tie)
     st, done = e.run(rule, 40)
     o = F64Tableau(T, {"cost_tie": tie, "ratio_tie": tie})
