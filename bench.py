@@ -348,11 +348,19 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
         e.set_block(block)
     block = engs[0].get_block()          # the auto choice (--block 0) resolved
     upload(engs, kind, m, ns, spans)
+    xw0 = engs[0].xwait()
     elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(engs[0], steps, warmup, block, lambda: None, every)
+    xw1 = engs[0].xwait()
     path, fallbacks = engs[0].exchange_path()
     geo = engs[0].geometry()
     acc = accounting(steps, block, elapsed, sw_ms, sel_ms, spans[0][1] - spans[0][0] + 1, n)
     acc["selection_kernel"] = geo["kernel"]
+    if geo.get("xcd_shards"):
+        # k_sel as one row shard per XCD: the shards' exchange per pivot
+        # (shard 0's block 0: its summary published -> every shard's seen)
+        acc["selection_kernel"] += f" as {geo['xcd_shards']} XCD row shards"
+        acc["xcd_hop_us_per_pivot"] = (1e6 * (xw1[0] - xw0[0]) / (xw1[1] - xw0[1])
+                                       if xw1[1] > xw0[1] else 0.0)
     acc.update(block=block, path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks,
                sweep_avg_us=sw_ms * 1e3, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
                selection_avg_launch_us=sel_ms * 1e3)
@@ -507,7 +515,7 @@ def main():
             "step_frac": acc["sweep_bytes_per_launch"] / (acc["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "traffic": traffic,
             "traffic_note": ("PMC FETCH_SIZE x2 + WRITE_SIZE per launch, measured on a build of these "
-                             "sources (profiles/r02/hbm_traffic.json, src_sha256)" if traffic else
+                             f"sources ({os.path.relpath(args.traffic_json, ROOT)}, src_sha256)" if traffic else
                              "not measured on a build of these sources / this workload"),
             "bytes_per_launch": acc["sweep_bytes_per_launch"],
             "avg_launch_us": sweep_ms * 1e3,
@@ -525,6 +533,7 @@ def main():
             "pivots_per_launch": B,
             "time_share": acc["selection_time_share"],
             **({"xrank_hop_us_per_pivot": acc["xrank_hop_us_per_pivot"]} if world > 1 else {}),
+            **({"xcd_hop_us_per_pivot": acc["xcd_hop_us_per_pivot"]} if "xcd_hop_us_per_pivot" in acc else {}),
         },
         "fallbacks": acc["fallbacks"],
         "src_sha256": digest,

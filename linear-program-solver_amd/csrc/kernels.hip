@@ -2030,8 +2030,14 @@ template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-           int nstrips, long long run)
+           int nstrips, long long run, long long tail, long long tcol)
 {
+    // tail > 0: the grid covers strips [0, nstrips) of the columns and the 64
+    // columns from tcol (the tableau's last columns: n + 1 is rarely a
+    // multiple of 64 W; the pitch's padding columns are 0 and stay 0, never
+    // swept) are dealt out `tail` rows to every block, one 8-row batch per
+    // wave -- a strip of its own would give those few columns a whole block
+    // per row run (cfg4: 30 of 510 resident slots)
     constexpr int RW = 8;                        // rows per batch
     constexpr int NC = NB / 2;                   // multiplier registers (2 pivots x 8 rows each)
     constexpr int XS = W * RW * 64;              // doubles of a slot's rows (W waves x 8 rows x 64 columns)
@@ -2055,18 +2061,24 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     const long long colw = (long long)strip * 64 * W + 64 * wave;
     const long long col = min(colw + (lane & ~1), ld - 2) + (lane & 1);
     const bool cok = colw + lane < ld;
+    // the tail piece of this block: rows [t0, t1), column tc of each lane
+    const long long t0 = (long long)blockIdx.x * tail, t1 = tail > 0 ? min(rows, t0 + tail) : 0;
+    const long long tc = min(tcol + lane, ld - 1);
+    const bool tok = tcol + lane < ld;
     if (nd != NB) {
         // a partial group (a call's last, or a stop inside it): pivot by
         // pivot from memory -- rare, never on the timed path
         __syncthreads();
-        for (long long row = r0; row < r1; ++row) {
-            double x = T[row * ld + col];
+        auto one = [&](long long row, long long c, bool ok) {
+            double x = T[row * ld + c];
             for (int s = 0; s < nd; ++s) {
-                if (sr[s] == row) x = P[(long long)s * ld + col];      // the pivot row becomes P[s]
-                else x = fma(-M[mq(row, s)], P[(long long)s * ld + col], x);
+                if (sr[s] == row) x = P[(long long)s * ld + c];        // the pivot row becomes P[s]
+                else x = fma(-M[mq(row, s)], P[(long long)s * ld + c], x);
             }
-            if (cok) Tout[row * ld + col] = x;
-        }
+            if (ok) Tout[row * ld + c] = x;
+        };
+        for (long long row = r0; row < r1; ++row) one(row, col, cok);
+        for (long long row = t0 + wave; row < t1; row += W) one(row, tc, tok);
         return;
     }
     double p[NB];
@@ -2171,6 +2183,41 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         for (int s = 0; s < NB; ++s)
             if (s > s0) y = fma(-M[mq(row, s)], p[s], y);
         if (cok) Tout[row * ld + col] = y;
+    }
+    if (t0 >= t1) return;                        // block-uniform: no tail piece
+    // ---- the tail piece: the 64 columns from tcol (one per lane) of rows
+    //      [t0, t1), wave w on batches t0 + 8 w, t0 + 8 (w + W), ...: the same
+    //      register FMAs with every operand loaded from memory (a few batches
+    //      per block)
+#pragma unroll
+    for (int s = 0; s < NB; ++s) p[s] = P[(long long)s * ld + tc];
+    for (long long rb = t0 + RW * wave; rb < t1; rb += RW * W) {
+        const int kmax = (int)min((long long)RW - 1, t1 - 1 - rb);
+        const int kr = min(vk, kmax);
+        double x[RW], m[NC];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) x[k] = T[(rb + min(k, kmax)) * ld + tc];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) m[c] = M[mq(rb + kr, 2 * c + vh)];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
+        if (tok) {
+#pragma unroll
+            for (int k = 0; k < RW; ++k) Tout[(rb + min(k, kmax)) * ld + tc] = x[k];
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int s0 = 0; s0 < nd; ++s0) {
+        const long long row = sr[s0];
+        if (row < t0 || row >= t1 || (row - t0) / RW % W != wave) continue;   // the wave that stored it
+        double y = p[0];
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            if (s == s0) y = p[s];
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            if (s > s0) y = fma(-M[mq(row, s)], p[s], y);
+        if (tok) Tout[row * ld + tc] = y;
     }
 }
 
@@ -2476,7 +2523,18 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         const void *fn = w8 ? RL_FN(8) : RL_FN(4);
 #undef RL_FN
         const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
-        const long long nsg = (A.ld + 64 * WL - 1) / (64 * WL);
+        // the columns swept: 0..n (the padding past them is 0 and stays 0).
+        // Whole strips of 64 WL columns; a last partial strip of <= 64
+        // columns is dealt out to every block (tail) -- LPGPU_SWEEP_TAIL=0:
+        // a strip of its own
+        static int rl_tail = -1;
+        if (rl_tail < 0) {
+            const char *v = std::getenv("LPGPU_SWEEP_TAIL");
+            rl_tail = v ? std::atoi(v) : 1;
+        }
+        const long long ncol = A.n + 1, nfull = ncol / (64 * WL), rest = ncol - nfull * 64 * WL;
+        const bool spread = rl_tail != 0 && nfull >= 1 && rest > 0 && rest <= 64;
+        const long long nsg = spread ? nfull : (ncol + 64 * WL - 1) / (64 * WL);
         const long long slots = (long long)sweep_cus() * bpc;
         long long nrun = slots / nsg;
         if (nrun < 1) nrun = 1;
@@ -2484,13 +2542,15 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         run = (run + 7) / 8 * 8;                 // whole 8-row batches (the multipliers' quads)
         nrun = (A.rows + run - 1) / run;
         const dim3 grid((unsigned)(nrun * nsg));
+        long long tail = spread ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + 7) / 8 * 8 : 0;
+        long long tcol = nfull * 64 * WL;
         const double *T = A.T, *Pp = A.P, *Mp = A.MQ;
         double *To = A.T;
         const long long *dRp = A.dR;
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
         int grpv = grp, nsv = (int)nsg;
-        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run};
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol};
         const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
         return err != hipSuccess ? err : hipGetLastError();
     }

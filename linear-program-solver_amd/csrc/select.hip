@@ -1043,6 +1043,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 status = LP_DEVICE_ERROR;
                 break;
             }
+            SEL_CLK(14);
             const double lp = lane < XS_SHARDS ? mk_d(x[0], x[1]) : INFINITY;
             const double gg = wmin(lp);
             if (!(gg < INFINITY)) {

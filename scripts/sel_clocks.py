@@ -32,8 +32,8 @@ buf = (C.c_longlong * (256 * BMAX * 4))()
 assert e.lib.lpdiag_bstamps(e.h, buf) == 0
 G = geo["blocks"]
 names = {1: "issue", 2: "colload", 3: "colchain", 4: "ratio", 5: "rpub", 6: "rgather", 7: "leave",
-         8: "rowload", 9: "rowchain", 10: "div", 11: "rowfin+epub", 12: "tail", 13: "egather", 0: "decide"}
-order = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 0]
+         8: "rowload", 9: "rowchain", 10: "div", 11: "rowfin+epub", 12: "tail", 13: "egather", 0: "decide", 14: "xshard"}
+order = [1, 2, 3, 4, 5, 6, 7, 14, 8, 9, 10, 11, 12, 13, 0]
 per = []
 clk = []
 for b in range(G):
