@@ -207,7 +207,10 @@ constexpr int GRAN_REGIONS = 4;       // regions of Args::gran (see there)
 // (their leaving-row summaries and straddle answers)
 constexpr int XS_SHARDS = 8;          // XCD shards of one device (MI355X: 8 XCDs)
 constexpr long long GRAN_SHARD = (long long)GRAN_REGIONS * GROUP_MAXBLOCKS * 8;
-constexpr long long GRAN_TOTAL = (XS_SHARDS + 1) * GRAN_SHARD;
+// common region: one replica per reading shard, XS_READER_STRIDE apart (a
+// summary polled by 64 blocks per line instead of 512 all on one line)
+constexpr long long XS_READER_STRIDE = 1032;
+constexpr long long GRAN_TOTAL = (XS_SHARDS + 2) * GRAN_SHARD;
 constexpr int GROUP_MINBLOCKS = 64;    // a small tableau still spreads its columns over 64 blocks
 constexpr int GROUP_THREADS = 64;      // one wave: block reductions stay in registers
 constexpr int GROUP_MAXRPL = 4;        // own rows per lane (<= 64 x 256 x 4 = 65536 rows per device, as LDS allows)

@@ -465,6 +465,15 @@ constexpr int SEL_NGR = 9;   // ratio summary: l (2), i, a (2), b (2), q of the 
 constexpr int SEL_NGE = 8;   // row-0 summary: l (2), q (2), i, fneg, P[t][i] (2)
 constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
 constexpr int SEL_NGX = 7;   // XR rank summary: l (2), global row, a (2), b (2)
+// XS: the shards' summaries are written to one replica per reading shard
+// (A/B build -DXS_SINGLE: one copy that all 512 blocks poll)
+#ifdef XS_SINGLE
+constexpr int XS_NREP = 1;
+#define XS_RD(s) 0
+#else
+constexpr int XS_NREP = XS_SHARDS;
+#define XS_RD(s) (s)
+#endif
 
 // pivot TQ's deferred register work (sel_body): its multiplier into m<TQ / 16>
 // [TQ % 16] -- every vector takes a select at the index, in place (a branch
@@ -588,7 +597,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     u64 *const grR = vgpr(gset);
     u64 *const grE = vgpr(gset + GROUP_MAXBLOCKS * GSLOT);
     u64 *const grS = vgpr(gset + 3 * GROUP_MAXBLOCKS * GSLOT);
-    u64 *const xsum = vgpr(A.gran + XS_SHARDS * GRAN_SHARD);
+    u64 *const xsum = vgpr(A.gran + XS_SHARDS * GRAN_SHARD);   // + reader shard x XS_READER_STRIDE
     ERec *const erecv = vgpr(A.erec);
     long long *const logv = vgpr(A.log);
     long long *const dRv = vgpr(A.dR);
@@ -1026,7 +1035,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             //      shard inside the global band (rows are shard-ordered, so
             //      that is the reference's first row)
             const int par = t & 1;
-            u64 *const xsl = xsum + par * 128;
+            u64 *const xsl = xsum + XS_RD(shard) * XS_READER_STRIDE + par * 128;   // this shard's replica
             if (b == 0 && lane < SEL_NGX) {
                 unsigned wv = R == NONE ? 0xffffffffu : (unsigned)(R - 1);
                 wv = wl(wv, lo32(g), 0);
@@ -1035,7 +1044,10 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 wv = wl(wv, hi32(aR), 4);
                 wv = wl(wv, lo32(bR), 5);
                 wv = wl(wv, hi32(bR), 6);
-                st_sc1(&xsl[lane * XS_SHARDS + shard], ((u64)gtag(seq, t, 2) << 32) | wv);
+                const u64 v = ((u64)gtag(seq, t, 2) << 32) | wv;
+#pragma unroll
+                for (int r = 0; r < XS_NREP; ++r)
+                    st_sc1(&xsum[r * XS_READER_STRIDE + par * 128 + lane * XS_SHARDS + shard], v);
             }
             unsigned x[SEL_NGX];
             const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
@@ -1062,7 +1074,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 // rare: a near-tie straddles the band across shards.  Shard
                 // ps's blocks each offer their first own row inside it (its
                 // rescan slots), its block 0 publishes the lowest to all
-                u64 *const xst = xsum + 256 + par * 8;
+                u64 *const xst = xsum + XS_RD(shard) * XS_READER_STRIDE + 256 + par * 8;
                 if ((int)shard == ps) {
                     const u64 mk = __ballot(okq && q <= thr);
                     const int fr = mk ? __builtin_ctzll(mk) : 0;
@@ -1088,7 +1100,10 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                         wv = wl(wv, rl32(wlo[0][2], bf), 2);
                         wv = wl(wv, rl32(wlo[0][3], bf), 3);
                         wv = wl(wv, rl32(wlo[0][4], bf), 4);
-                        st_sc1(&xst[lane], ((u64)gtag(seq, t, 5) << 32) | wv);
+                        const u64 v = ((u64)gtag(seq, t, 5) << 32) | wv;
+#pragma unroll
+                        for (int r = 0; r < XS_NREP; ++r)
+                            st_sc1(&xsum[r * XS_READER_STRIDE + 256 + par * 8 + lane], v);
                     }
                 }
                 unsigned y[SEL_NGS];
