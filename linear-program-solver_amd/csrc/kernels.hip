@@ -2522,6 +2522,17 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         const int WL = w8 ? 8 : 4;
         const void *fn = w8 ? RL_FN(8) : RL_FN(4);
 #undef RL_FN
+        // batches in flight at 64 pivots, 8 waves: the 254-VGPR kernel runs one
+        // workgroup per CU, so 4 (three batches ahead: 108 KB of LDS) instead
+        // of 2 (cfg4, same-box A/B: 902-918 against 916-959 us per launch);
+        // LPGPU_SWEEP_D=2/3 for A/B
+        static int dl_env = -1;
+        if (dl_env < 0) {
+            const char *v = std::getenv("LPGPU_SWEEP_D");
+            dl_env = v ? std::atoi(v) : 4;
+        }
+        if (w8 && nb == 64 && dl_env == 3) fn = (const void *)&k_sweep_rl<8, 64, 3, SA>;
+        if (w8 && nb == 64 && dl_env == 4) fn = (const void *)&k_sweep_rl<8, 64, 4, SA>;
         const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
         // the columns swept: 0..n (the padding past them is 0 and stays 0).
         // Whole strips of 64 WL columns; a last partial strip of <= 64
