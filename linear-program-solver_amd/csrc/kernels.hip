@@ -2531,6 +2531,12 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
             const char *v = std::getenv("LPGPU_SWEEP_D");
             dl_env = v ? std::atoi(v) : 4;
         }
+        static int dl4_env = -1;
+        if (dl4_env < 0) {
+            const char *v = std::getenv("LPGPU_SWEEP_D4");   // A/B: the same for 4 waves
+            dl4_env = v ? std::atoi(v) : DL;
+        }
+        if (!w8 && nb == 64 && dl4_env == 3) fn = (const void *)&k_sweep_rl<4, 64, 3, SA>;
         if (w8 && nb == 64 && dl_env == 3) fn = (const void *)&k_sweep_rl<8, 64, 3, SA>;
         if (w8 && nb == 64 && dl_env == 4) fn = (const void *)&k_sweep_rl<8, 64, 4, SA>;
         const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
