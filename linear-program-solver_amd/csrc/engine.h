@@ -173,7 +173,10 @@ struct Args {
 // exchange buffer layout (granules of 8 bytes), see kernels.hip (XR)
 constexpr int NRANK_MAX = 64;
 constexpr long long XS_SUM_PAR = (NRANK_MAX + 1) * 8;            // per parity
-constexpr long long XS_PROW = 2 * XS_SUM_PAR;
+// the summary slots in XS_SHARDS replicas, one per XCD shard of a rank that
+// runs k_sel<XR, XS> (every other selection kernel uses replica 0)
+constexpr long long XS_XREP = 2 * XS_SUM_PAR;
+constexpr long long XS_PROW = 8 * XS_XREP;
 constexpr long long XS_PROW_BLOCK = 2 * 4 * 64;                   // 2 granules x 4 columns x 64 lanes
 constexpr long long XS_PROW_RANK = 256 * XS_PROW_BLOCK;           // GROUP_MAXBLOCKS blocks per source rank
 // + 2 parities x nranks x XS_PROW_RANK of pivot-row slices, then the local

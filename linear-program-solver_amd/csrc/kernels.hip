@@ -2710,7 +2710,7 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, in
     }
     // the one-XCD selection k_sel (select.hip) where the shape fits it
     if (xcd_on && xr != 1 && nshard == 1 && share == 1) {
-        const GroupGeom S = sel_geom(rc, n, bmax, sweep_cus() / 8, xr != 0, xs_ok && xr == 0);
+        const GroupGeom S = sel_geom(rc, n, bmax, sweep_cus() / 8, xr != 0, xs_ok && xr != 1);
         if (S.g > 0) return S;
     }
     static long long gmin_env = -1;

@@ -936,7 +936,8 @@ static lpk::GroupGeom persistent_geom_b(lp_handle *h, size_t nmem, int *xr, int 
     if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
     *xr = (nmem == 1 && h->xr_xcd) ? 2 : 1;
-    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 && *xr != 2 ? h->share : 1);
+    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 && *xr != 2 ? h->share : 1,
+                           h->xs_ok);
 }
 
 // Pivots per sweep when the handle says auto (0).  More pivots per sweep cut

@@ -512,7 +512,6 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                                          double *lP, long long npiv, long long nstd, long long stuck, int rule,
                                          const unsigned shard)
 {
-    static_assert(!(XR && XS), "k_sel: XS is one device");
     constexpr int CS = NB + 2;             // LDS stride of a column's pivot values (16-B reads, no conflicts)
     constexpr int NK = NB / 16;            // broadcast registers
     const int lane = threadIdx.x;
@@ -880,154 +879,11 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             SEL_DONE(pv[IPL - 1]);
             SEL_CLK(10);
         };
+        double gR = g;                        // the device's minimum (XS: over its shards)
+        double lps = INFINITY;                // XS: lane x < 8 holds shard x's minimum
         bool win = true;                      // this rank holds the leaving row
         long long rglob = R == NONE ? -1 : R - 1 + rbv;
-        if constexpr (XR) {
-            // ---- leaving row across ranks (as k_group): every rank sends
-            //      (local minimum, global row, pivot element, b) to all ranks
-            //      and, without waiting for the verdict, its candidate's
-            //      normalised row on every block's columns
-            const int par = t & 1;
-            const int N = A.nranks;                 // (a uniform loop bound: kept scalar)
-            const unsigned long long xticks = (unsigned long long)A.xwait_ms * 100000ull;
-            u64 *xsl = xbufv + par * XS_SUM_PAR;
-            if (b == 0 && lane < SEL_NGX) {
-                const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
-                unsigned wv = R == NONE ? 0xffffffffu : (unsigned)rglob;
-                wv = wl(wv, lo32(g), 0);
-                wv = wl(wv, hi32(g), 1);
-                wv = wl(wv, lo32(aR), 3);
-                wv = wl(wv, hi32(aR), 4);
-                wv = wl(wv, lo32(bR), 5);
-                wv = wl(wv, hi32(bR), 6);
-                for (int p = 0; p < N; ++p)
-                    st_sys(&(*gp(peerv + p))[par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
-            }
-            auto send_row = [&](int ph) {
-                const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
-                for (int p = 0; p < N; ++p) {
-                    if (p == A.rank) continue;
-                    u64 *dst = (*gp(peerv + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
-                               (long long)b * XS_PROW_BLOCK;
-#pragma unroll
-                    for (int k = 0; k < IPL; ++k) {
-                        const int kk = lane + 64 * k;
-                        if (cok[k]) {
-                            st_sys(&dst[2 * kk], tg | lo32(pv[k]));
-                            st_sys(&dst[2 * kk + 1], tg | hi32(pv[k]));
-                        }
-                    }
-                }
-            };
-            if (R != NONE) {
-                prow(R, aR);
-                send_row(3);
-            }
-            unsigned x[SEL_NGX];
-            const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
-            if (!gather_x<SEL_NGX>(xsl, N, gtag(seq, t, 2), x, &ctlv->bar_timeout, xticks)) {
-                status = LP_DEVICE_ERROR;
-                break;
-            }
-            const double lp = lane < N ? mk_d(x[0], x[1]) : INFINITY;
-            const double gg = wmin(lp);
-            if (!(gg < INFINITY)) {
-                status = LP_UNBOUNDED;
-                break;
-            }
-            const double thr = tie_band(gg, tol.ratio_tie);
-            const int ps = __builtin_ctzll(__ballot(lane < N && lp <= thr));
-            double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
-            bool okp;
-            const double qs = row_ratio(as, bs, tol, okp);
-            long long rg;
-            int ph = 3;                       // the tag of the winner's row slices
-            if (okp && qs <= thr) {
-                rg = (long long)rl32(x[2], ps);
-            } else {
-                // rare: a near-tie straddles the band across ranks.  Rank ps
-                // finds its first row inside it (each block offers its first
-                // own row, block 0 sends the lowest to every rank) and ships
-                // that row's normalised values instead of its candidate's
-                if (A.rank == ps) {
-                    const u64 mk = __ballot(okq && q <= thr);
-                    const int fr = mk ? __builtin_ctzll(mk) : 0;
-                    const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
-                    u64 *loc = xbufv + XS_PROW + 2LL * N * XS_PROW_RANK;
-                    if (lane < SEL_NGS) {
-                        unsigned wv = mk ? (unsigned)(lr0 + fr) : 0x7fffffffu;
-                        wv = wl(wv, lo32(ar), 1);
-                        wv = wl(wv, hi32(ar), 2);
-                        wv = wl(wv, lo32(br), 3);
-                        wv = wl(wv, hi32(br), 4);
-                        st_sc1(&loc[b * 8 + lane], ((u64)gtag(seq, t, 4) << 32) | wv);
-                    }
-                    unsigned wlo[1][SEL_NGS];
-                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wlo, &ctlv->bar_timeout, spin)) {
-                        status = LP_DEVICE_ERROR;
-                        break;
-                    }
-                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
-                    const unsigned r0w = rl32(wlo[0][0], bf), a0 = rl32(wlo[0][1], bf), a1 = rl32(wlo[0][2], bf),
-                                   b0 = rl32(wlo[0][3], bf), b1 = rl32(wlo[0][4], bf);
-                    if (b == 0 && lane < SEL_NGS) {
-                        unsigned wv = (unsigned)((long long)r0w - 1 + rbv);
-                        wv = wl(wv, a0, 1);
-                        wv = wl(wv, a1, 2);
-                        wv = wl(wv, b0, 3);
-                        wv = wl(wv, b1, 4);
-                        for (int p = 0; p < N; ++p)
-                            st_sys(&(*gp(peerv + p))[par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
-                                   ((u64)gtag(seq, t, 5) << 32) | wv);
-                    }
-                }
-                unsigned y[SEL_NGS];
-                if (!gather_x<SEL_NGS>(xsl + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctlv->bar_timeout, xticks)) {
-                    status = LP_DEVICE_ERROR;
-                    break;
-                }
-                rg = (long long)__builtin_amdgcn_readfirstlane(y[0]);
-                as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
-                bs = mk_d(__builtin_amdgcn_readfirstlane(y[3]), __builtin_amdgcn_readfirstlane(y[4]));
-                ph = 6;
-                if (A.rank == ps) {
-                    prow(rg - rbv + 1, as);
-                    send_row(6);
-                }
-            }
-            win = A.rank == ps;
-            rglob = rg;
-            R = win ? rg - rbv + 1 : -1;
-            aR = as;
-            bR = bs;
-            if (!win) {
-                // the winning rank's block b sent these columns
-                const u64 *src = xbufv + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
-                                 (long long)b * XS_PROW_BLOCK;
-                const unsigned tg = gtag(seq, t, ph);
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                for (;;) {
-                    bool ok = true;
-#pragma unroll
-                    for (int k = 0; k < IPL; ++k) {
-                        const int kk = kc[k];
-                        const u64 lo = ld_sys(&src[2 * kk]), hi = ld_sys(&src[2 * kk + 1]);
-                        pv[k] = mk_d((unsigned)lo, (unsigned)hi);
-                        ok = ok && (!cok[k] || ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
-                    }
-                    if (__all(ok)) break;
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
-                        st_sc1(&ctlv->bar_timeout, 1u);
-                        status = LP_DEVICE_ERROR;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(SEL_SLEEP);
-                }
-                if (status != LP_PIVOTED) break;
-            }
-            xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
-            p0 = bR / aR;
-        } else if constexpr (XS) {
+        if constexpr (XS) {
             // ---- leaving row across the XCD shards: block 0 of every shard
             //      publishes (shard minimum, row, pivot element, b), write-
             //      through, granule-major (one poll instruction reads granule
@@ -1058,11 +914,15 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             SEL_CLK(14);
             const double lp = lane < XS_SHARDS ? mk_d(x[0], x[1]) : INFINITY;
             const double gg = wmin(lp);
+            lps = lane < XS_SHARDS ? lp : INFINITY;
             if (!(gg < INFINITY)) {
-                status = LP_UNBOUNDED;
-                break;
+                if constexpr (!XR) {
+                    status = LP_UNBOUNDED;
+                    break;
+                }
             }
             const double thr = tie_band(gg, tol.ratio_tie);
+            if (gg < INFINITY) {
             const int ps = __builtin_ctzll(__ballot(lane < XS_SHARDS && lp <= thr));
             double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
             bool okp;
@@ -1115,15 +975,180 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
                 bs = mk_d(__builtin_amdgcn_readfirstlane(y[3]), __builtin_amdgcn_readfirstlane(y[4]));
             }
-            rglob = rg;
+            rglob = rg + rbv;
             R = rg + 1;
             aR = as;
             bR = bs;
-            xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
+            gR = gg;
+            } else {
+                R = NONE;                     // XR: no candidate on this device
+                gR = INFINITY;
+            }
+            if (status != LP_PIVOTED) break;
+            if constexpr (!XR) xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
             // every shard: the pivot row on its blocks' columns from the
-            // stored row and the leaving row's multipliers (write-through)
-            prow(R, aR);
-        } else {
+            // stored row and the leaving row's multipliers (write-through);
+            // XR: the device's candidate, computed in the cross-rank step
+            if constexpr (!XR) prow(R, aR);
+        }
+        if constexpr (XR) {
+            // ---- leaving row across ranks (as k_group): every rank sends
+            //      (local minimum, global row, pivot element, b) to all ranks
+            //      and, without waiting for the verdict, its candidate's
+            //      normalised row on every block's columns
+            const int par = t & 1;
+            const int N = A.nranks;                 // (a uniform loop bound: kept scalar)
+            const unsigned long long xticks = (unsigned long long)A.xwait_ms * 100000ull;
+            // (XS: the rank's candidate is its shards' (above); the summaries
+            // go to one replica per XCD shard of every rank, and each peer's
+            // copy of the pivot row is sent by one of the shards)
+            constexpr int NREP = XS ? XS_SHARDS : 1;
+            u64 *xsl = xbufv + (XS ? (long long)shard * XS_XREP : 0) + par * XS_SUM_PAR;
+            if (b == 0 && lane < SEL_NGX && shard == 0) {
+                const unsigned long long tg = (u64)gtag(seq, t, 2) << 32;
+                unsigned wv = R == NONE ? 0xffffffffu : (unsigned)rglob;
+                wv = wl(wv, lo32(gR), 0);
+                wv = wl(wv, hi32(gR), 1);
+                wv = wl(wv, lo32(aR), 3);
+                wv = wl(wv, hi32(aR), 4);
+                wv = wl(wv, lo32(bR), 5);
+                wv = wl(wv, hi32(bR), 6);
+                for (int p = 0; p < N; ++p)
+#pragma unroll
+                    for (int r = 0; r < NREP; ++r)
+                        st_sys(&(*gp(peerv + p))[r * XS_XREP + par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
+            }
+            auto send_row = [&](int ph) {
+                const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
+                for (int p = 0; p < N; ++p) {
+                    if (p == A.rank) continue;
+                    if (XS && ((p - A.rank + N) % N - 1) % XS_SHARDS != (int)shard) continue;
+                    u64 *dst = (*gp(peerv + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
+                               (long long)b * XS_PROW_BLOCK;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        const int kk = lane + 64 * k;
+                        if (cok[k]) {
+                            st_sys(&dst[2 * kk], tg | lo32(pv[k]));
+                            st_sys(&dst[2 * kk + 1], tg | hi32(pv[k]));
+                        }
+                    }
+                }
+            };
+            if (R != NONE) {
+                prow(R, aR);
+                send_row(3);
+            }
+            unsigned x[SEL_NGX];
+            const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
+            if (!gather_x<SEL_NGX>(xsl, N, gtag(seq, t, 2), x, &ctlv->bar_timeout, xticks)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
+            const double lp = lane < N ? mk_d(x[0], x[1]) : INFINITY;
+            const double gg = wmin(lp);
+            if (!(gg < INFINITY)) {
+                status = LP_UNBOUNDED;
+                break;
+            }
+            const double thr = tie_band(gg, tol.ratio_tie);
+            const int ps = __builtin_ctzll(__ballot(lane < N && lp <= thr));
+            double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
+            bool okp;
+            const double qs = row_ratio(as, bs, tol, okp);
+            long long rg;
+            int ph = 3;                       // the tag of the winner's row slices
+            if (okp && qs <= thr) {
+                rg = (long long)rl32(x[2], ps);
+            } else {
+                // rare: a near-tie straddles the band across ranks.  Rank ps
+                // finds its first row inside it (each block offers its first
+                // own row, block 0 sends the lowest to every rank) and ships
+                // that row's normalised values instead of its candidate's
+                // (XS: the rank's first shard whose minimum lies inside the
+                // band holds that row: its blocks offer, its block 0 sends)
+                const int sfirst = XS ? __builtin_ctzll(__ballot(lane < XS_SHARDS && lps <= thr) | (1ull << 63)) : 0;
+                if (A.rank == ps && (int)shard == sfirst) {
+                    const u64 mk = __ballot(okq && q <= thr);
+                    const int fr = mk ? __builtin_ctzll(mk) : 0;
+                    const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
+                    u64 *loc = XS ? grS + 1536 : xbufv + XS_PROW + 2LL * N * XS_PROW_RANK;
+                    if (lane < SEL_NGS) {
+                        unsigned wv = mk ? (unsigned)(lr0 + fr) : 0x7fffffffu;
+                        wv = wl(wv, lo32(ar), 1);
+                        wv = wl(wv, hi32(ar), 2);
+                        wv = wl(wv, lo32(br), 3);
+                        wv = wl(wv, hi32(br), 4);
+                        st_sc1(&loc[b * 8 + lane], ((u64)gtag(seq, t, 4) << 32) | wv);
+                    }
+                    unsigned wlo[1][SEL_NGS];
+                    if (!gather<1, SEL_NGS, false>(loc, G, gtag(seq, t, 4), wlo, &ctlv->bar_timeout, spin)) {
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
+                    const unsigned r0w = rl32(wlo[0][0], bf), a0 = rl32(wlo[0][1], bf), a1 = rl32(wlo[0][2], bf),
+                                   b0 = rl32(wlo[0][3], bf), b1 = rl32(wlo[0][4], bf);
+                    if (b == 0 && lane < SEL_NGS) {
+                        unsigned wv = (unsigned)((long long)r0w - 1 + rbv);
+                        wv = wl(wv, a0, 1);
+                        wv = wl(wv, a1, 2);
+                        wv = wl(wv, b0, 3);
+                        wv = wl(wv, b1, 4);
+                        for (int p = 0; p < N; ++p)
+#pragma unroll
+                            for (int r = 0; r < NREP; ++r)
+                                st_sys(&(*gp(peerv + p))[r * XS_XREP + par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
+                                       ((u64)gtag(seq, t, 5) << 32) | wv);
+                    }
+                }
+                unsigned y[SEL_NGS];
+                if (!gather_x<SEL_NGS>(xsl + NRANK_MAX * 8, 1, gtag(seq, t, 5), y, &ctlv->bar_timeout, xticks)) {
+                    status = LP_DEVICE_ERROR;
+                    break;
+                }
+                rg = (long long)__builtin_amdgcn_readfirstlane(y[0]);
+                as = mk_d(__builtin_amdgcn_readfirstlane(y[1]), __builtin_amdgcn_readfirstlane(y[2]));
+                bs = mk_d(__builtin_amdgcn_readfirstlane(y[3]), __builtin_amdgcn_readfirstlane(y[4]));
+                ph = 6;
+                if (A.rank == ps) {
+                    prow(rg - rbv + 1, as);
+                    send_row(6);
+                }
+            }
+            win = A.rank == ps;
+            rglob = rg;
+            R = win ? rg - rbv + 1 : -1;
+            aR = as;
+            bR = bs;
+            if (!win) {
+                // the winning rank's block b sent these columns
+                const u64 *src = xbufv + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
+                                 (long long)b * XS_PROW_BLOCK;
+                const unsigned tg = gtag(seq, t, ph);
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    bool ok = true;
+#pragma unroll
+                    for (int k = 0; k < IPL; ++k) {
+                        const int kk = kc[k];
+                        const u64 lo = ld_sys(&src[2 * kk]), hi = ld_sys(&src[2 * kk + 1]);
+                        pv[k] = mk_d((unsigned)lo, (unsigned)hi);
+                        ok = ok && (!cok[k] || ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
+                    }
+                    if (__all(ok)) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
+                        st_sc1(&ctlv->bar_timeout, 1u);
+                        status = LP_DEVICE_ERROR;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(SEL_SLEEP);
+                }
+                if (status != LP_PIVOTED) break;
+            }
+            xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
+            p0 = bR / aR;
+        } else if constexpr (!XS) {
             prow(R, aR);
         }
         // ---- P[t], row 0 and column 0 (every block: p0 = b / a).  P[t] is
@@ -1418,9 +1443,12 @@ const void *sel_kernel(int ipl, int nb, bool xr, bool xs)
 #define SEL_K(I, N) (xr ? reinterpret_cast<const void *>(&k_sel<I, N, true, false>) \
                         : reinterpret_cast<const void *>(&k_sel<I, N, false, false>))
 #define SEL_XS(I) reinterpret_cast<const void *>(&k_sel<I, 64, false, true>)
-    if (xs) return nb != 64 || xr ? nullptr : ipl == 1 ? SEL_XS(1) : ipl == 2 ? SEL_XS(2) : SEL_XS(4);
+#define SEL_XR_XS(I) reinterpret_cast<const void *>(&k_sel<I, 64, true, true>)
+    if (xs && xr) return nb != 64 ? nullptr : ipl == 1 ? SEL_XR_XS(1) : ipl == 2 ? SEL_XR_XS(2) : SEL_XR_XS(4);
+    if (xs) return nb != 64 ? nullptr : ipl == 1 ? SEL_XS(1) : ipl == 2 ? SEL_XS(2) : SEL_XS(4);
     if (nb == 32) return ipl == 1 ? SEL_K(1, 32) : ipl == 2 ? SEL_K(2, 32) : SEL_K(4, 32);
     return ipl == 1 ? SEL_K(1, 64) : ipl == 2 ? SEL_K(2, 64) : SEL_K(4, 64);
+#undef SEL_XR_XS
 #undef SEL_XS
 #undef SEL_K
 }
@@ -1457,7 +1485,7 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
     int xs = 0;
     long long rps = rc;
     if ((rc + 63) / 64 > 64) {
-        if (!xs_ok || xr || bmax <= 32) return G;
+        if (!xs_ok || bmax <= 32) return G;
         xs = XS_SHARDS;
         rps = (rc + XS_SHARDS - 1) / XS_SHARDS;
     }
@@ -1505,7 +1533,7 @@ hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int gr
 {
     if (geo.g == 0 || geo.sel == 0 || count < 1 || count > geo.sel) return hipErrorInvalidValue;
     if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
-    if (geo.xs && (geo.xs != XS_SHARDS || xr)) return hipErrorInvalidValue;
+    if (geo.xs && geo.xs != XS_SHARDS) return hipErrorInvalidValue;
     if (A.rc > 64 * geo.g * (geo.xs ? XS_SHARDS : 1) || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
     const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0, geo.xs > 0);
     if (!fn) return hipErrorInvalidValue;

@@ -50,6 +50,8 @@ def main():
     if os.environ.get("EXPECT_KERNEL"):        # which selection kernel the persistent path ran
         geo = e.geometry()
         assert geo["kernel"] == os.environ["EXPECT_KERNEL"], (rank, geo)
+        if os.environ.get("EXPECT_XS"):            # k_sel<XR> as XCD shards inside the rank
+            assert geo["xcd_shards"] == 8 and geo["xcd_shards_engaged"], (rank, geo)
     want = _lib.PATH_PEER if mode not in ("host", "fault") and world <= 4 else _lib.PATH_COLLECTIVE
     # "fault": rank 0's first persistent launch withholds a summary (LPGPU_FAULT);
     # every rank times out in that group, the ranks agree on it and all redo it

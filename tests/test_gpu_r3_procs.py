@@ -79,3 +79,37 @@ def test_one_xcd_cross_rank_selection(kind, m, ns, k, block, tie):
         outs.append(out.decode(errors="replace"))
     for p, out in zip(procs, outs):
         assert p.returncode == 0, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,m,ns,k,block,tie", [
+    ("tall", 8400, 40, 90, 64, 1e-12),           # 4200 rows per rank: 8 shards of 525
+    ("tall", 8400, 40, 70, 0, 1e-12),            # auto pivots per sweep
+    ("tall", 9000, 60, 60, 64, 0.25),            # wide tie band: straddles across ranks and shards
+])
+def test_xcd_shards_cross_rank_selection(kind, m, ns, k, block, tie):
+    """ranks taller than one XCD (2 and 4 GPUs of cfg4: 16384 / 8192 rows per
+    rank): k_sel<XR, XS>, the rank's XCD shards exchange inside the device and
+    the rank's candidate and pivot row go to the other ranks.  Two processes
+    forced onto the one box (LPGPU_XR_XCD=1; narrow tableaux, so both ranks'
+    launches are resident together), bit-exact against oracle/lp_f64.c"""
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                   WORLD_SIZE="2", LOCAL_RANK="0", LPGPU_XR_XCD="1", LPGPU_STRICT="1", EXPECT_KERNEL="k_sel",
+                   EXPECT_XS="1")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(HERE, "_peer_worker.py"), kind, str(m), str(ns), str(k), str(block),
+             str(tie), "peer"], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
