@@ -2563,6 +2563,13 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         long long tcol = nfull * 64 * WL;
         const double *T = A.T, *Pp = A.P, *Mp = A.MQ;
         double *To = A.T;
+#ifdef SWEEP_OOP_PROBE
+        // timing probe only (results are NOT kept): the sweep writes a scratch
+        // copy instead of the tableau, to time an out-of-place pass
+        static double *scratch = nullptr;
+        if (!scratch && hipMalloc(&scratch, (size_t)A.rows * A.ld * sizeof(double)) != hipSuccess) scratch = nullptr;
+        if (scratch) To = scratch;
+#endif
         const long long *dRp = A.dR;
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
