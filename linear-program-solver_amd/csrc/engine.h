@@ -267,6 +267,9 @@ hipError_t launch_group(hipStream_t s, const Args &A, const GroupGeom &geo, int 
                         int from_erec, unsigned seq, int bmax, int xr, const Args *As, int nshard,
                         int first, int fmode, int frule, long long fcap, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr);
+// a persistent selection launch (cooperative unless LPGPU_COOP=0)
+hipError_t launch_persistent(const void *fn, dim3 grid, void **args, size_t lds, hipStream_t s, hipEvent_t e0,
+                             hipEvent_t e1);
 // row-sharded: every rank writes a tagged granule to every rank's buffer and
 // waits (bounded) for all of them; *ok = 1 | flags OR << 1 if all arrived
 hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev);

@@ -2843,7 +2843,32 @@ hipError_t launch_group(hipStream_t s, const Args &A, const GroupGeom &geo, int 
     int gper = (int)geo.g;
     void *args[] = {&a0, &as, &gper, &grp, &count, &from_erec, &seq, &bmax,
                     const_cast<int *>(&xmode), &first, &fmode, &frule, &fcap};
-    return hipExtLaunchKernel(fn, grid, dim3(GROUP_THREADS), args, geo.lds, s, e0, e1, 0);
+    return launch_persistent(fn, grid, args, geo.lds, s, e0, e1);
+}
+
+// A persistent selection launch (k_group, k_sel): its blocks wait on each
+// other, so all must be resident at once -- sized from the compiled kernel's
+// occupancy (group_geom / sel_geom), with every exchange bounded (a group
+// that is not resident times out and is redone on the per-pivot kernels).
+// LPGPU_COOP=1: a cooperative launch instead, which the runtime admits only
+// if every block fits at once (hipErrorCooperativeLaunchTooLarge otherwise);
+// tests/test_gpu_r3.py runs the suite's persistent geometries that way to
+// check the sizing against the runtime's admission.  Not the default: same
+// speed on the bench (cfg4 46.3-46.6k against 46.6-46.7k pivots/s) but 25-35
+// us more per call on small LPs (cfg1 41-54 -> 77-83 us).
+hipError_t launch_persistent(const void *fn, dim3 grid, void **args, size_t lds, hipStream_t s, hipEvent_t e0,
+                             hipEvent_t e1)
+{
+    static int coop = -1;
+    if (coop < 0) {
+        const char *v = std::getenv("LPGPU_COOP");
+        coop = v ? std::atoi(v) : 0;
+    }
+    if (!coop) return hipExtLaunchKernel(fn, grid, dim3(GROUP_THREADS), args, lds, s, e0, e1, 0);
+    hipError_t err = e0 ? hipEventRecord(e0, s) : hipSuccess;
+    if (err == hipSuccess) err = hipLaunchCooperativeKernel(fn, grid, dim3(GROUP_THREADS), args, lds, s);
+    if (err == hipSuccess && e1) err = hipEventRecord(e1, s);
+    return err;
 }
 
 hipError_t launch_resume(hipStream_t s, const Args &A)

@@ -1541,7 +1541,7 @@ hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int gr
     Args a0 = A;
     int gper = (int)geo.g;
     void *args[] = {&a0, &gper, &grp, &count, &from_erec, &seq, &first, &fmode, &frule, &fcap};
-    return hipExtLaunchKernel(fn, grid, dim3(GROUP_THREADS), args, geo.lds, s, e0, e1, 0);
+    return launch_persistent(fn, grid, args, geo.lds, s, e0, e1);
 }
 
 }  // namespace lpk

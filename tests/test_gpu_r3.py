@@ -212,3 +212,46 @@ def test_tall_40000_rows_persistent():
         assert e.log().tolist() == olog.tolist()
         assert np.array_equal(e.download(), o.T)
         e.close()
+
+
+_COOP_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1] + "/linear-program-solver_amd", sys.argv[1]]
+from lpsol_amd import _lib, generators as gen
+from oracle.f64 import F64Tableau
+_lib.load()
+kind, m, ns, block, kernel = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
+T = gen.tableau(kind, m, ns, 9)
+e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+e.upload(T)
+e.set_block(block)
+st, done = e.run(_lib.RULE_STANDARD, 70)
+o = F64Tableau(T)
+ost, olog = o.run(0, 70)
+assert e.log().tolist() == olog.tolist()
+assert np.array_equal(e.download(), o.T)
+assert e.exchange_path() == (_lib.PATH_PERSISTENT, 0), e.exchange_path()
+assert e.geometry()["kernel"] == kernel, e.geometry()
+print("ok", e.geometry())
+"""
+
+
+@pytest.mark.parametrize("kind,m,ns,block,kernel", [
+    ("mixed", 4096, 4096, 0, "k_sel"),     # cfg3's one-XCD geometry
+    ("tall", 32768, 8192, 0, "k_sel"),     # cfg4's XCD shards (512 blocks, 2 per CU)
+    ("tall", 36000, 300, 64, "k_group"),   # k_group spread, two rows per lane
+    ("tall", 40000, 64, 64, "k_group"),    # four rows per lane
+])
+def test_persistent_geometry_admitted_by_cooperative_launch(kind, m, ns, block, kernel):
+    """the occupancy sizing of every persistent selection kind, checked by the
+    runtime: LPGPU_COOP=1 launches them cooperatively, which the runtime
+    refuses (hipErrorCooperativeLaunchTooLarge -> LP_DEVICE_ERROR) unless every
+    block of the grid is resident at once; results bit-exact, no fallback"""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LPGPU_COOP="1", LPGPU_STRICT="1")
+    r = subprocess.run([sys.executable, "-c", _COOP_CHILD, root, kind, str(m), str(ns), str(block), kernel],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
