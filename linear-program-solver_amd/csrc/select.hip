@@ -1,7 +1,9 @@
 // One-XCD persistent pivot selection (k_sel): every selection of a group of
 // chained pivots in ONE launch whose G <= 64 single-wave workgroups share one
 // XCD -- the cfg3 tableau (4096 x 8192) on one GPU, and each rank's 4096-row
-// shard of cfg4 across eight (BASELINE.json north_star).
+// shard of cfg4 across eight (BASELINE.json north_star).  k_sel<XS>: a
+// tableau of up to 8 x 4096 rows (cfg4 on one GPU, or one rank of 2 / 4 GPUs
+// with XR) as 8 such row shards in one launch, one per XCD (sel_body).
 //
 // Same contract as k_group (kernels.hip), rebuilt around what bounds a pivot
 // there -- a chain of dependent latencies (two block exchanges, two dependent
