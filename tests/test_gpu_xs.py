@@ -156,3 +156,26 @@ def test_xs_and_k_group_agree_with_explicit_pivots():
         want.run(0, 20)
         assert np.array_equal(e.download(), want.T)
         e.close()
+
+
+def test_xs_frontend_simplex_solve():
+    """the lpsol-compatible front-end on a tableau taller than one XCD:
+    Simplex.solve (simplex.py:110-148) runs lp_solve on the XCD shards and
+    replays the device log through _pivot; the basis follows the oracle's
+    pivot sequence, the objective and the downloaded tableau match it"""
+    from lpsol_amd import Simplex, Tableau
+    T = gen.tableau("pos", 4500, 60, 50)
+    tab = Tableau.fromArray(T)
+    s = Simplex(tab)
+    s.solve()
+    o = F64Tableau(T)
+    ost, olog, _ = o.solve()
+    eng = tab._engine()
+    assert eng.log().tolist() == olog.tolist()
+    assert eng.geometry()["xcd_shards"] == 8
+    assert abs(s.getObjValue() - o.objective()) <= 1e-9 * max(1.0, abs(o.objective()))
+    assert np.array_equal(tab.toArray(), o.T)
+    bfs = list(range(T.shape[1] - 1 - (T.shape[0] - 1), T.shape[1] - 1))   # the slacks start basic
+    for r, c in olog.tolist():
+        bfs[r] = c
+    assert s.getBasicSequence() == bfs
