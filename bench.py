@@ -7,7 +7,8 @@
 A pivot is the reference's ``findPivotStandard(True)``: entering-column scan,
 min-ratio test and the rank-1 elimination of the whole float64 tableau
 (``lpsol/simplex.py:251-284``, ``lpsol/tableau.py:295-308``).  The engine
-selects ``block`` pivots (default 32) from current values and then applies
+selects ``block`` pivots (default: the engine's automatic depth, 64 on cfg3
+and cfg4) from current values and then applies
 their eliminations to the stored tableau in ONE pass (bit-identical to
 immediate updates).  One STEP is one such group: ``block`` pivots selected
 plus one elimination pass over the whole tableau, so ``--steps K`` times

@@ -164,6 +164,11 @@ struct Args {
     int fault;           // tests only (LPGPU_FAULT): t + 1 -> block 1 withholds pivot t's ratio summary
     int hier;            // k_group: two-level exchange when the blocks are spread over the XCDs (1) or flat (0)
     int rank;            // this rank (row-sharded jobs)
+    // one-XCD k_sel (not XS): -1 the blocks 0, 8, 16, ... work (whichever XCD
+    // block 0 lands on); 0..7 the blocks that find themselves on XCD xtarget
+    // work -- ranks sharing one GPU each take their own XCD (lpgpu.cpp)
+    int xtarget;
+    int fault_xcc;       // tests only (LPGPU_FAULT_XCC): block 1 (shard 0) reports another XCD
     // row-sharded persistent selection: this rank's exchange buffer and every
     // rank's (peer[rank] == xbuf), written by the peers over xGMI
     unsigned long long *xbuf;
@@ -197,9 +202,12 @@ hipError_t launch_ratio(hipStream_t s, const Args &A, int t, int grp, int mode, 
 hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
-// T <- T with the group's pivots, in place; nd_max >= ndef
-// (e0, e1: events recorded at the kernel's start and end, for lp_profile)
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0 = nullptr,
+// T <- T with the group's pivots, in place; nd_max >= ndef: the handle's
+// pivots per sweep; cnt (> 0): the most pivots this group can hold, when the
+// host knows it (a call's last group, an explicit pivot) -- a shallower
+// kernel then, or the padded k_sweep_rl (e0, e1: events recorded at the
+// kernel's start and end, for lp_profile)
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int cnt = -1, hipEvent_t e0 = nullptr,
                         hipEvent_t e1 = nullptr);
 
 constexpr int GROUP_MAXBLOCKS = 256;
@@ -254,7 +262,10 @@ GroupGeom group_geom(long long rc, long long ld, long long n, int bmax, int xr, 
 // the variable columns 1..n split evenly; g == 0 if the shape does not fit.
 // xs_ok (single device): a tableau too tall for one XCD may run as XS_SHARDS
 // row shards of <= 64 g rows, one per XCD, in one launch (geo.xs)
-GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok);
+// share: ranks of a job on this GPU whose launches must be resident together
+// (XR; the one-XCD kernel puts each on its own XCD, Args::xtarget, the XCD
+// shards need share x g blocks on every XCD)
+GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok, int share = 1);
 hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int grp, int count, int from_erec,
                       unsigned seq, int xr, int first, int fmode, int frule, long long fcap, hipEvent_t e0,
                       hipEvent_t e1);

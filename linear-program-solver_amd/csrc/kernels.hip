@@ -1972,28 +1972,31 @@ __device__ __forceinline__ void rg_pair(double (&x)[8], double m, double pa, dou
 #undef RGF
 
 // ---------------------------------------------------------------------------
-// K3 (registers + LDS streaming): k_sweep_rl (LPGPU_SWEEP_DP=5, A/B).  The
-//   DPP sweeps above read P from LDS for every pivot of every batch (16 bytes
-//   per lane per 8 FMAs: more LDS bandwidth per FMA than a CU has at full
-//   FMA rate).  Here the pivot rows stay in registers and no operand of an FMA
-//   comes from LDS: the tableau rows and the multipliers travel HBM -> LDS
-//   with global_load_lds_dwordx4 (no VGPRs), D batches deep, and each batch is
-//   read into registers once:
+// K3 (registers + LDS streaming): k_sweep_rl -- THE sweep of every group of
+//   49..64 pivots (launch_sweep: the automatic depth is 64 for cfg3 and cfg4,
+//   so this is the bench's update kernel; k_sweep_dp2 serves 17..48 and the
+//   per-pivot path's 32).  The DPP sweeps above read P from LDS for every
+//   pivot of every batch (16 bytes per lane per 8 FMAs: more LDS bandwidth per
+//   FMA than a CU has at full FMA rate).  Here the pivot rows stay in
+//   registers and no operand of an FMA comes from LDS: the tableau rows and
+//   the multipliers travel HBM -> LDS with global_load_lds_dwordx4 (no VGPRs),
+//   D batches deep, and each batch is read into registers once:
 //     * a workgroup of W waves owns a strip of 64 W columns (one per lane) of a
 //       run of rows; all W waves take the SAME 8-row batch, each on its own 64
 //       columns, so the batch's multipliers (two MQ quads, 4 KB) are copied
 //       once per workgroup -- one dwordx4 per wave;
-//     * each wave keeps P[0..NB) of its column in registers;
+//     * each wave keeps P[0..NB) of its column in registers (2 NB VGPRs);
 //     * per batch: wait for its copies (vmcnt, one workgroup barrier), start the
 //       copies of batch i + D - 1 into the slot batch i - 1 used, read x (8
 //       rows) and the multipliers' DPP registers from LDS, the FMAs, store x.
-//   Every element gets exactly upd()'s float64 operations in pivot order:
-//   bit-identical to oracle/lp_f64.c (the GPU suite passes with it).
-//   Measured (cfg3, profiles/r03/README.md): no faster than k_sweep_dp /
-//   k_sweep_dp2 (151.7 against 149.7 us at 64 pivots, 118.3 against 113.2 at
-//   48; scripts/fma_probe.hip rules out the FMA issue rate: 55 TFLOP/s at two
-//   waves per SIMD), so the DPP sweeps stay the default.  (A first version
-//   with the rows in VGPRs, one batch in flight per wave, reached 0.41 of HBM.)
+//   A group the host knows to be short (49..63 pivots) runs the same pass
+//   with the missing pivots' rows of P and multipliers zeroed by the host
+//   (exact no-ops); shorter ones take k_sweep_dp2 at their own depth
+//   (launch_sweep).  Every element gets exactly
+//   upd()'s float64 operations in pivot order: bit-identical to
+//   oracle/lp_f64.c.  cfg4 (W = 8, D = 4, 254 VGPRs, one workgroup per CU):
+//   884 us per 64-pivot launch = 0.61 of the HBM spec; cfg3 (W = 4, D = 2):
+//   139 us = 0.49 (profiles/r03/kernel_stats_r03_final.csv).
 // ---------------------------------------------------------------------------
 // LDS byte offset of a __shared__ location (for LDS accesses written in asm)
 __device__ __forceinline__ unsigned lds_off(const double *p)
@@ -2030,7 +2033,7 @@ template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-           int nstrips, long long run, long long tail, long long tcol)
+           int nstrips, long long run, long long tail, long long tcol, int nexp)
 {
     // tail > 0: the grid covers strips [0, nstrips) of the columns and the 64
     // columns from tcol (the tableau's last columns: n + 1 is rarely a
@@ -2055,9 +2058,9 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
     const long long r1 = min(rows, r0 + run);
     // this lane's column.  Lanes past the pitch (the last strip of a pitch
-    // that is not a multiple of 64 W) take the column their LDS position was
-    // copied from (ld - 2 or ld - 1) and store the same values as its owner,
-    // so every wave issues the same instructions (the waits count them)
+    // that is not a multiple of 64 W: whole waves) load from column ld - 2 /
+    // ld - 1 and their stores are dropped (below), so every wave issues the
+    // same instructions (the waits count them)
     const long long colw = (long long)strip * 64 * W + 64 * wave;
     const long long col = min(colw + (lane & ~1), ld - 2) + (lane & 1);
     const bool cok = colw + lane < ld;
@@ -2065,9 +2068,12 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     const long long t0 = (long long)blockIdx.x * tail, t1 = tail > 0 ? min(rows, t0 + tail) : 0;
     const long long tc = min(tcol + lane, ld - 1);
     const bool tok = tcol + lane < ld;
-    if (nd != NB) {
-        // a partial group (a call's last, or a stop inside it): pivot by
-        // pivot from memory -- rare, never on the timed path
+    if (nd != nexp) {
+        // a group that stopped early (the solve ended inside it: once per
+        // call) -- pivot by pivot from memory.  A group the host knows to be
+        // short of NB (nexp < NB: a call's last, a depth of 49..63) runs the
+        // full pass: the host zeroed its pivot rows and multipliers past nexp
+        // (launch_sweep), so those pivots are exact no-ops, fma(-0, 0, x) == x
         __syncthreads();
         auto one = [&](long long row, long long c, bool ok) {
             double x = T[row * ld + c];
@@ -2136,8 +2142,8 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");   // D == 4, i == 2
         }
         __syncthreads();                         // every wave's copies of batch i are in LDS
-        issue(min(i + D - 1, nbat - 1));         // into the slot batch i - 1 used (all waves past it)
         const int slot = (int)(i % D);
+        issue(min(i + D - 1, nbat - 1));         // into the slot batch i - 1 used (all waves past it)
         const long long rb = r0 + i * RW;
         const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
         double x[RW], m[NC];
@@ -2152,6 +2158,12 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             lds_rows<RW>(x, xa);
             lds_mult<NC>(m, ma);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // the loaded registers as outputs of asm ordered after the wait:
+            // nothing that reads them (FMAs, the padding select) moves above it
+#pragma unroll
+            for (int k = 0; k < RW; ++k) asm volatile("" : "+v"(x[k]));
+#pragma unroll
+            for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(m[c]));
         } else {
 #pragma unroll
             for (int k = 0; k < RW; ++k) x[k] = xs[slot][(wave * RW + min(k, kmax)) * 64 + lane];
@@ -2162,9 +2174,15 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
 #pragma unroll
         for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
         {
-            // write-through stores (SA), as the DPP sweeps'
-            const __amdgpu_buffer_rsrc_t ro = buf_rsrc(Tout + rb * ld + colw);
-            const int voff = (int)(col - colw) * 8, ldb = (int)(ld * 8);
+            // write-through stores (SA), as the DPP sweeps'.  A wave whose 64
+            // columns lie past the pitch (ld is a multiple of 64, so a wave is
+            // wholly inside or wholly past it) stores through a resource of 0
+            // records: the hardware drops every one of its stores, and the
+            // wave still issues them (its vmcnt waits count them)
+            const bool wok = __builtin_amdgcn_readfirstlane((int)cok) != 0;
+            const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+                Tout + rb * ld + colw, (short)0, wok ? 0x7fffffff : 0, 0x00020000);
+            const int voff = lane * 8, ldb = (int)(ld * 8);
 #pragma unroll
             for (int k = 0; k < RW; ++k)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, x[k]), ro, voff, min(k, kmax) * ldb, SA);
@@ -2487,14 +2505,17 @@ static int sweep_blocks_per_cu(const void *fn, int threads)
     return n;
 }
 
-// The sweep: k_sweep_st (8 waves x 4-row batches), write-through (sc1)
-// stores -- the tableau lines leave the L2 as they are written instead of in
-// the writeback at the kernel's end (sweep 104-106 vs 106.5-108.4 us per
-// launch at cfg3, profiles/r01/README.md).  As many row runs as fill three
-// workgroups per CU at <= 32 pivots (the strip's slice of P takes NB KB of
-// LDS: two at 48, one at 64).
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEvent_t e0, hipEvent_t e1)
+// The sweep launch.  Which kernel (LPGPU_SWEEP_DP=1, the default): k_sweep_rl
+// for groups of 49..64 pivots (the automatic depth of cfg3 and cfg4 is 64, so
+// it is the bench's kernel), k_sweep_dp2 for 17..48 (and the per-pivot
+// path's 32); k_sweep_dp / k_sweep_st stay as A/B variants.  All stores are
+// write-through (sc1): the tableau lines leave the L2 as they are written
+// instead of in the writeback at the kernel's end (profiles/r01/README.md).
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int cnt, hipEvent_t e0, hipEvent_t e1)
 {
+    // the kernel's depth: the group's known pivot count when the host knows it
+    // (a call's last group, explicit pivots), else the handle's depth
+    if (cnt > 0 && cnt < nd_max) nd_max = cnt;
     constexpr int W = 8, RW = 4, SA = 16;
     // LPGPU_SWEEP_DP (A/B): 1 (default) k_sweep_dp2 up to 48 pivots per sweep and
     // k_sweep_rl at 64 (round 3: cfg4 906-931 against 978-980 us per launch,
@@ -2523,7 +2544,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         const void *fn = w8 ? RL_FN(8) : RL_FN(4);
 #undef RL_FN
         // batches in flight at 64 pivots, 8 waves: the 254-VGPR kernel runs one
-        // workgroup per CU, so 4 (three batches ahead: 108 KB of LDS) instead
+        // workgroup per CU, so 4 (three batches ahead: 144 KB of LDS) instead
         // of 2 (cfg4, same-box A/B: 902-918 against 916-959 us per launch);
         // LPGPU_SWEEP_D=2/3 for A/B
         static int dl_env = -1;
@@ -2539,6 +2560,18 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         if (!w8 && nb == 64 && dl4_env == 3) fn = (const void *)&k_sweep_rl<4, 64, 3, SA>;
         if (w8 && nb == 64 && dl_env == 3) fn = (const void *)&k_sweep_rl<8, 64, 3, SA>;
         if (w8 && nb == 64 && dl_env == 4) fn = (const void *)&k_sweep_rl<8, 64, 4, SA>;
+        // a group of nexp = 49..63 pivots: the pivot rows and multipliers
+        // past it zeroed (stale rows of an earlier group otherwise; rows of
+        // P and entries of MQ that no selection of this group writes), so
+        // the pass treats them as exact no-ops
+        int nexp = nd_max < nb ? nd_max : nb;
+        if (nexp < nb) {
+            hipError_t e = hipMemsetAsync(A.P + (long long)nexp * A.ld, 0, (size_t)(nb - nexp) * A.ld * 8, s);
+            if (e == hipSuccess)
+                e = hipMemset2DAsync(A.MQ + nexp * 4, 4 * BMAX * 8, 0, (size_t)(nb - nexp) * 4 * 8,
+                                     (size_t)((A.rows + 3) / 4), s);
+            if (e != hipSuccess) return e;
+        }
         const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
         // the columns swept: 0..n (the padding past them is 0 and stays 0).
         // Whole strips of 64 WL columns; a last partial strip of <= 64
@@ -2574,7 +2607,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, hipEv
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
         int grpv = grp, nsv = (int)nsg;
-        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol};
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &nexp};
         const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
         return err != hipSuccess ? err : hipGetLastError();
     }
@@ -2716,8 +2749,10 @@ static GroupGeom group_geom_uncached(long long rc, long long ld, long long n, in
         xcd_on = v ? std::atoi(v) : 1;
     }
     // the one-XCD selection k_sel (select.hip) where the shape fits it
-    if (xcd_on && xr != 1 && nshard == 1 && share == 1) {
-        const GroupGeom S = sel_geom(rc, n, bmax, sweep_cus() / 8, xr != 0, xs_ok && xr != 1);
+    // (ranks sharing a GPU: only the XR variant that may use one XCD, which
+    // then sizes for the co-located ranks itself)
+    if (xcd_on && xr != 1 && nshard == 1 && (share == 1 || xr == 2)) {
+        const GroupGeom S = sel_geom(rc, n, bmax, sweep_cus() / 8, xr != 0, xs_ok && xr != 1, share);
         if (S.g > 0) return S;
     }
     static long long gmin_env = -1;

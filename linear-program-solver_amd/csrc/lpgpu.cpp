@@ -52,6 +52,7 @@ struct lp_handle {
     unsigned spin_max = 1u << 22;   // polls of one k_group exchange before it gives up
     unsigned xwait_ms = 30000;      // bound of a cross-rank wait (XR)
     int fault_launch = 0, fault_t = 0;   // tests: LPGPU_FAULT=<launch>:<pivot>
+    int fault_xcc = 0;              // tests: LPGPU_FAULT_XCC=<launch> (a block of k_sel reports another XCD)
     bool strict = false;            // LPGPU_STRICT=1 (tests): a timed-out group is an error
     bool xs_ok = true;              // a tall single-device tableau may take k_sel's XCD shards
                                     // (LPGPU_SEL_XS=0 / lpdiag_set_xcd_shards: k_group instead)
@@ -61,6 +62,7 @@ struct lp_handle {
     std::vector<void *> ipc_open;           // peer buffers opened from IPC handles
     bool peer_ok = false;                   // the exchange is set up and validated
     bool xr_xcd = false;                    // every rank on its own GPU: one-XCD selection
+    int xtarget = -1;                       // k_sel's XCD when ranks share a GPU (Args::xtarget)
     int share = 1;                          // most ranks of the job on one GPU (from the ping)
     bool peer_enable = true;                // LPGPU_PEER=0 keeps the RCCL per-pivot path
     int last_path = 0;                      // lp_exchange_path of the last pivot loop
@@ -311,6 +313,8 @@ static Args args_of(const lp_handle *h)
     }();
     A.hier = hier;
     A.rank = h->rank;
+    A.xtarget = h->xtarget;
+    A.fault_xcc = 0;
     A.xbuf = h->xbuf;
     A.peer = h->dpeer;
     return A;
@@ -391,6 +395,7 @@ static int alloc_handle(lp_handle *h)
     if (const char *v = std::getenv("LPGPU_SPIN_MAX")) h->spin_max = (unsigned)std::strtoul(v, nullptr, 10);
     if (const char *v = std::getenv("LPGPU_XWAIT_MS")) h->xwait_ms = (unsigned)std::strtoul(v, nullptr, 10);
     if (const char *v = std::getenv("LPGPU_FAULT")) std::sscanf(v, "%d:%d", &h->fault_launch, &h->fault_t);
+    if (const char *v = std::getenv("LPGPU_FAULT_XCC")) h->fault_xcc = std::atoi(v);
     if (const char *v = std::getenv("LPGPU_STRICT")) h->strict = v[0] == '1';
     if (const char *v = std::getenv("LPGPU_SEL_XS")) h->xs_ok = v[0] != '0';
     if (const char *pe = std::getenv("LPGPU_PEER")) h->peer_enable = pe[0] != '0';
@@ -675,12 +680,17 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     h->share = 1;
     while (h->share < 8 && (bits >> h->share)) ++h->share;
     h->xr_xcd = h->share == 1;
+    h->xtarget = -1;
     if (const char *v = std::getenv("LPGPU_XR_XCD")) {
         // A/B and tests: 0 off; 1 on even for ranks sharing a GPU (tests of
-        // the one-XCD cross-rank selection k_sel<XR> on one box: small
-        // tableaux, whose ranks' blocks all fit on the one XCD together)
+        // the one-XCD cross-rank selection k_sel<XR> on one box).  Ranks
+        // sharing a GPU then each take their own XCD (Args::xtarget: rank % 8,
+        // distinct for up to 8 ranks), so each rank's launch needs only its
+        // own XCD's slots -- the same residency as one rank per GPU; more than
+        // 8 ranks on one GPU keep the spread kernels
         if (v[0] == '0') h->xr_xcd = false;
-        if (v[0] == '1') h->xr_xcd = true;
+        if (v[0] == '1') h->xr_xcd = h->share == 1 || h->nranks <= 8;
+        if (h->xr_xcd && h->share > 1) h->xtarget = h->rank % 8;
     }
     return LP_PIVOTED;
 }
@@ -886,11 +896,13 @@ static int prof_slot(lp_handle *h, hipEvent_t *e0, hipEvent_t *e1, int kind)
     return LP_PIVOTED;
 }
 
-static int launch_sweep_timed(lp_handle *h, const Args &A, int grp)
+// cnt: the most pivots the group can hold (the kernel's depth when below the
+// handle's: a call's last group, an explicit pivot)
+static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, int cnt)
 {
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 0));
-    HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), e0, e1));
+    HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), cnt, e0, e1));
     return LP_PIVOTED;
 }
 
@@ -912,6 +924,7 @@ static int launch_group_timed(lp_handle *h, const Args &A, const lpk::GroupGeom 
     CALL(prof_slot(h, &e0, &e1, 1));
     Args a = A;
     if (h->fault_launch > 0 && (unsigned)h->fault_launch == h->gseq) a.fault = h->fault_t + 1;
+    if (h->fault_xcc > 0 && (unsigned)h->fault_xcc == h->gseq) a.fault_xcc = 1;
     HCHK(h, lpk::launch_group(h->s, a, geo, grp, cnt, from_erec, h->gseq, block_of(h), xr, As, nshard,
                               cs.first, cs.mode, cs.rule, cs.cap, e0, e1));
     return LP_PIVOTED;
@@ -936,20 +949,19 @@ static lpk::GroupGeom persistent_geom_b(lp_handle *h, size_t nmem, int *xr, int 
     if (!h->peer_ok || h->share > 4) return none;
     const int64_t rcmax = (h->m + h->nranks - 1) / h->nranks;
     *xr = (nmem == 1 && h->xr_xcd) ? 2 : 1;
-    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 && *xr != 2 ? h->share : 1,
-                           h->xs_ok);
+    return lpk::group_geom(rcmax, h->ld, h->n, bmax, *xr, (int)nmem, nmem == 1 ? h->share : 1, h->xs_ok);
 }
 
 // Pivots per sweep when the handle says auto (0).  More pivots per sweep cut
 // the sweep's traffic per pivot, but each selection block keeps its rows'
 // multipliers and its columns' pivot-row values in LDS, so past some depth
-// the persistent selection no longer fits on one XCD (its L2-resident
-// hand-offs) and gets slower: the deepest of 64 / 48 / 32 whose selection
-// still runs on one XCD; 64 where none does (a tall shard spread over the
-// device anyway: cfg4 on one GPU, 31.6-32.0k pivots/s at 64 against 28.8k at
-// 48); 32 on the per-pivot kernels.  cfg3 (4096 x 8192): 48, 100-101k
-// against 97-98k at 32 and 80k at 64 (profiles/r02/README.md).  Every rank
-// of a sharded job decides from the same global sizes.
+// the persistent selection may no longer fit on one XCD (its L2-resident
+// hand-offs): the deepest of 64 / 48 / 32 whose selection still runs on one
+// XCD (or as k_sel's XCD shards); 64 where none does (a tall shard spread over
+// the device anyway); 32 on the per-pivot kernels.  Since round 3's k_sel,
+// cfg3 (4096 x 8192) and cfg4 (32768 x 8192) both take 64 (cfg3: 146-148k
+// pivots/s, profiles/r03/README.md).  Every rank of a sharded job decides
+// from the same global sizes.
 static int block_of(lp_handle *h)
 {
     if (h->block > 0) return h->block;
@@ -1075,9 +1087,9 @@ static int enqueue_select(const Members &M, const std::vector<Args> &A, int t, i
     return LP_PIVOTED;
 }
 
-static int enqueue_sweep(const Members &M, const std::vector<Args> &A, int grp)
+static int enqueue_sweep(const Members &M, const std::vector<Args> &A, int grp, int cnt)
 {
-    for (size_t k = 0; k < M.size(); ++k) CALL(launch_sweep_timed(M[k], A[k], grp));
+    for (size_t k = 0; k < M.size(); ++k) CALL(launch_sweep_timed(M[k], A[k], grp, cnt));
     return LP_PIVOTED;
 }
 
@@ -1215,7 +1227,9 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
         CALL(begin_call(M, A, mode, rule, 1, cap, -1, -1));
         for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
     }
-    const int B = block_of(h);
+    // (re-read after a timeout recovery: the per-pivot kernels take their own
+    // automatic depth, and the sweep launches ask block_of for theirs)
+    int B = block_of(h);
     int64_t done = 0;      // pivots performed (device count)
     int64_t batch = 2 * B;   // open-ended solves: few launches for a short solve, then doubling
     int grp = 0;
@@ -1238,7 +1252,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
                 CALL(enqueue_group(M, A, geo, xr, grp, cnt, chained ? 1 : 0, cs));
                 if (cs.first) first_seq = M[0]->gseq;
                 cs.first = 0;
-                CALL(enqueue_sweep(M, A, grp));
+                CALL(enqueue_sweep(M, A, grp, cnt));
                 grp ^= 1;
                 chained = true;
             }
@@ -1248,7 +1262,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
                 CALL(enqueue_select(M, A, t, grp, 0, chained ? 1 : 0, false, true));
                 chained = true;
                 if (++t == B || k + 1 == b) {
-                    CALL(enqueue_sweep(M, A, grp));
+                    CALL(enqueue_sweep(M, A, grp, t));
                     grp ^= 1;
                     t = 0;
                 }
@@ -1263,6 +1277,11 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             if (h->strict) return fail(h, LP_DEVICE_ERROR, "persistent selection group timed out (LPGPU_STRICT)");
             CALL(recover_timeout(M, A, mode, rule, cap, first_seq));
             geo = lpk::GroupGeom{};
+            // groups of the depth the sweeps now take (recover_timeout re-chose
+            // the automatic one for the per-pivot kernels): a group deeper than
+            // the sweep kernel's compiled bound would drop pivots
+            B = block_of(h);
+            batch = std::min<int64_t>(batch, std::max<int64_t>(1024, 32 * B));
             for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
             chained = false;
             grp = 0;
@@ -1274,7 +1293,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             // ctl->c holds its entering column; redo it with two exchanges
             for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_resume(M[k]->s, A[k]));
             CALL(enqueue_select(M, A, 0, grp, 0, 0, false, false));
-            CALL(enqueue_sweep(M, A, grp));
+            CALL(enqueue_sweep(M, A, grp, 1));
             grp ^= 1;
             CALL(sync_ctl(M));
         }
@@ -1315,7 +1334,7 @@ extern "C" int lp_find_pivot(lp_handle *h, int rule, int do_pivot, int64_t *r, i
     CALL(begin_call(M, A, lpk::MODE_RUN, rule, 0, -1, -1, -1));
     for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
     CALL(enqueue_select(M, A, 0, 0, 0, 0, do_pivot == 0));
-    if (do_pivot) CALL(enqueue_sweep(M, A, 0));
+    if (do_pivot) CALL(enqueue_sweep(M, A, 0, 1));
     CALL(sync_ctl(M));
     if (h->hctl->status == LP_PIVOTED) {
         *r = h->hctl->r;
@@ -1332,7 +1351,7 @@ static int explicit_pivot(lp_handle *h, int64_t r, int64_t c, bool checked)
     const std::vector<Args> A = args_all(M);
     CALL(begin_call(M, A, lpk::MODE_RUN, LP_RULE_STANDARD, 0, -1, r, c));
     CALL(enqueue_select(M, A, 0, 0, checked ? 1 : 2, 0, false));
-    CALL(enqueue_sweep(M, A, 0));
+    CALL(enqueue_sweep(M, A, 0, 1));
     CALL(sync_ctl(M));
     return h->hctl->status;
 }

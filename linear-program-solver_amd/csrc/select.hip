@@ -1379,7 +1379,12 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     // one XCD under the round-robin dealing of workgroups (checked below).
     // XS: every block works, block 8 b + x being block b of shard x (so each
     // shard's blocks share one XCD, checked below, and each XCD holds one shard)
-    if (!XS && (blockIdx.x & 7u)) return;
+    // (A.xtarget >= 0: the blocks that land on XCD xtarget work instead -- the
+    // same G blocks b = blockIdx.x / 8 under the round-robin dealing, on an
+    // XCD the host chose: ranks sharing one GPU take different ones)
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    if (!XS && (A.xtarget < 0 ? (blockIdx.x & 7u) != 0u : xcc != (unsigned)A.xtarget)) return;
     extern __shared__ __attribute__((aligned(16))) double lP[];   // [cpb][NB + 2]: P[s][own column]
     const unsigned b = blockIdx.x >> 3, G = (unsigned)gper;
     const unsigned shard = XS ? (blockIdx.x & 7u) : 0u;
@@ -1412,17 +1417,20 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         // (lpgpu.cpp recover_timeout).  (The eager row-0 copies of a call's
         // first launch are drained by its entering-column exchange, not by
         // this one.)
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        // (what is compared: the XCD and the block's residue mod 8, so that
+        // under XCD targeting the G working blocks are also one residue class,
+        // i.e. b = 0 .. G - 1 each exactly once)
+        unsigned me = xcc | ((blockIdx.x & 7u) << 8);
+        if (A.fault_xcc && b == min(1u, G - 1) && shard == 0) me ^= 1u;   // tests: a misplaced block
         u64 *const grX = A.gran + (XS ? (long long)shard * GRAN_SHARD : 0) + 2 * GROUP_MAXBLOCKS * GSLOT;
         drain_stores();
-        if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | xcc);
+        if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | me);
         unsigned wx[1];
         if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
             if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
             return;
         }
-        const bool same = !((unsigned)lane < G) || wx[0] == xcc;
+        const bool same = !((unsigned)lane < G) || wx[0] == me;
         if (!__all(same)) {
             if (b == 0 && lane == 0) {
                 *gp(&ctl->sel_flags) = 8u | 4u;
@@ -1473,7 +1481,7 @@ int sel_per_cu(const void *fn, size_t lds)
 
 }  // namespace
 
-GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok)
+GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok, int share)
 {
     GroupGeom G;
     static int on = -1;
@@ -1511,7 +1519,15 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
         if (std::getenv("LPGPU_GEOM_DEBUG"))
             fprintf(stderr, "sel_geom rc %lld n %lld bmax %d xs %d g %lld ipl %d lds %zu per_cu %d xcd_cus %d\n", rc,
                     n, bmax, xs, gc, ipl, lds, per_cu, xcd_cus);
-        if (per_cu >= 1 && gc <= (long long)per_cu * xcd_cus) {
+        // blocks this launch and the co-located ranks' need on one XCD at once.
+        // XCD shards: every block works, share x gc per XCD.  One XCD (each
+        // co-located rank on its own, Args::xtarget): gc, plus one free slot --
+        // the other ranks' grids deal 7 of every 8 blocks to XCDs they do not
+        // work on, and those idle blocks (exiting at once) still need a slot
+        // to pass through in dispatch order: with the XCD full, the other
+        // rank's launch stalls there and never reaches its own XCD
+        const long long need = xs ? gc * std::max(share, 1) : share > 1 ? gc + 1 : gc;
+        if (per_cu >= 1 && need <= (long long)per_cu * xcd_cus) {
             g = gc;
             break;
         }

@@ -52,6 +52,13 @@ def main():
         assert geo["kernel"] == os.environ["EXPECT_KERNEL"], (rank, geo)
         if os.environ.get("EXPECT_XS"):            # k_sel<XR> as XCD shards inside the rank
             assert geo["xcd_shards"] == 8 and geo["xcd_shards_engaged"], (rank, geo)
+        else:
+            assert geo["xcd_shards"] == 0 and geo["on_one_xcd"], (rank, geo)
+        if os.environ.get("EXPECT_GEOM"):          # "blocks,ipl" of the launch the rank ran
+            g, ipl = (int(x) for x in os.environ["EXPECT_GEOM"].split(","))
+            assert (geo["blocks"], geo["ipl"]) == (g, ipl), (rank, geo)
+    if os.environ.get("EXPECT_BLOCK"):            # the automatic pivots per sweep
+        assert e.get_block() == int(os.environ["EXPECT_BLOCK"]), (rank, e.get_block())
     want = _lib.PATH_PEER if mode not in ("host", "fault") and world <= 4 else _lib.PATH_COLLECTIVE
     # "fault": rank 0's first persistent launch withholds a summary (LPGPU_FAULT);
     # every rank times out in that group, the ranks agree on it and all redo it

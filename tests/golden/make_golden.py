@@ -6,6 +6,7 @@ Run from the repo root (needs /root/reference, read-only):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--big]
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --extra   # r2.json only
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline 10   # r3.json only
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline-prefix 64   # r4.json, checkpointed
 
 It imports the reference, drives its own ``Tableau``/``Simplex`` on inputs
 from this repo's generator (``lpsol_amd.generators``) or on hand-built LPs,
@@ -340,6 +341,43 @@ def headline_main(k: int):
         json.dump({"standard_k": [fx]}, f, separators=(",", ":"))
 
 
+def headline_prefix_main(k: int):
+    """tests/golden/r4.json: the same reference walk as ``headline_main`` on
+    the cfg3 bench tableau, extended towards one full 64-pivot bench group and
+    CHECKPOINTED: after every reference pivot the prefix so far (sequence and
+    exact objective ``-_z`` of the reference, ``tableau.py:82-84``) is written
+    atomically, so a run stopped after any number of pivots leaves a valid
+    fixture.  Several hours on one core (denominators grow with the pivots)."""
+    spec = {"gen": {"kind": "mixed", "m": 4096, "ns": 4096, "seed": 3}}
+    T, rows = source_of(spec)
+    t = ref_tableau_from_rows(rows)
+    del rows
+    log = []
+    s = bare_simplex(t, log)
+    path = os.path.join(OUT, "r4.json")
+    t0 = time.time()
+    end = None
+    times = []
+    for i in range(k):
+        res = s.findPivotStandard(True)
+        if isinstance(res, str):
+            end = res
+        times.append(round(time.time() - t0, 1))
+        fx = {
+            "name": "cfg3_mixed_4096x4096_s3_prefix", "mode": "standard_k", "k": len(log),
+            **spec, "m": int(T.shape[0] - 1), "n": int(T.shape[1] - 1),
+            "sha256": gen.digest(T), "seq": [[r, c] for r, c, _ in log], "end": end,
+            "objective": fs(t.getZ()), "objective_float": float(t.getZ()),
+            "ref_seconds": times[-1], "ref_seconds_cumulative": times,
+        }
+        with open(path + ".tmp", "w") as f:
+            json.dump({"standard_k": [fx]}, f, separators=(",", ":"))
+        os.replace(path + ".tmp", path)
+        print(f"pivot {len(log)}: {log[-1][:2] if log else None} at {times[-1]} s", flush=True)
+        if end is not None:
+            break
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true")
@@ -347,7 +385,13 @@ def main():
                     help="only tests/golden/r2.json (solve assertions, saveJson round trips)")
     ap.add_argument("--headline", type=int, default=0, metavar="K",
                     help="only tests/golden/r3.json: K reference pivots on the cfg3 bench tableau")
+    ap.add_argument("--headline-prefix", type=int, default=0, metavar="K",
+                    help="only tests/golden/r4.json: up to K reference pivots on the cfg3 bench "
+                         "tableau, rewritten after every pivot")
     args = ap.parse_args()
+    if args.headline_prefix:
+        headline_prefix_main(args.headline_prefix)
+        return
     if args.extra:
         extra_main()
         return

@@ -1,0 +1,153 @@
+"""Round 4 GPU tests (MI355X, through the C-ABI), from ADVICE r3:
+
+* a timed-out persistent group while the pivots per sweep are AUTOMATIC (64):
+  the host redoes the group on the per-pivot kernels, whose sweeps take their
+  own automatic depth (32) -- the pivot loop must group by that same depth
+  (lpgpu.cpp pivot_loop re-reads block_of after recover_timeout);
+* the XCD-placement abort of k_sel (Ctl::sel_flags 8): a block that reports
+  another XCD (LPGPU_FAULT_XCC) makes the launch give up; the host redoes the
+  group on the per-pivot kernels, one-XCD and XCD-shard launches;
+* groups the host knows to be short run full-speed passes (launch_sweep's
+  cnt): 49..63 pivots the k_sweep_rl pass with the missing pivots' P rows and
+  multipliers zeroed by the host, fewer k_sweep_dp2 at their own depth --
+  bit-identical (every bit, signed zeros included) to oracle/lp_f64.c.
+
+Reference: /root/reference/lpsol/tableau.py:295-308 (pivot),
+simplex.py:251-284 (findPivotStandard).
+"""
+import time
+
+import numpy as np
+import pytest
+
+from lpsol_amd import _lib
+from lpsol_amd import generators as gen
+from oracle.f64 import F64Tableau
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    _lib.load()
+    assert _lib.device_count() > 0, "no GPU visible"
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
+
+
+def _engine(T, block):
+    e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+    e.upload(T)
+    e.set_block(block)
+    return e
+
+
+@pytest.mark.parametrize("kind,m,ns,launch,t", [
+    ("mixed", 400, 800, 1, 3),       # one-XCD k_sel, the first launch
+    ("mixed", 400, 800, 2, 40),      # a later launch, deep in the group
+    ("tall", 9000, 48, 1, 5),        # k_sel's XCD shards
+])
+def test_timeout_recovery_at_automatic_depth(monkeypatch, kind, m, ns, launch, t):
+    """LPGPU_FAULT withholds a ratio summary in a group of
+    the automatic 64 pivots; the redone pivots run on the per-pivot kernels at
+    their automatic 32 -- sequence and tableau as without the fault"""
+    monkeypatch.setenv("LPGPU_FAULT", f"{launch}:{t}")
+    monkeypatch.setenv("LPGPU_SPIN_MAX", "20000")
+    monkeypatch.delenv("LPGPU_STRICT", raising=False)
+    T = gen.tableau(kind, m, ns, 17)
+    e = _engine(T, 0)
+    assert e.get_block() == 64 and e.geometry()["kernel"] == "k_sel"
+    k = 200
+    st, done = e.run(_lib.RULE_STANDARD, k)
+    o = F64Tableau(T)
+    ost, olog = o.run(0, k)
+    assert (st, done) == (ost, len(olog))
+    assert e.log().tolist() == olog.tolist()
+    assert _bits_equal(e.download(), o.T)
+    assert e.exchange_path() == (_lib.PATH_KERNELS, 1)
+    assert e.get_block() == 32                       # the per-pivot kernels' depth
+    e.close()
+
+
+@pytest.mark.parametrize("kind,m,ns,block,launch", [
+    ("mixed", 400, 800, 64, 2),      # one-XCD k_sel, the second launch
+    ("mixed", 400, 800, 0, 2),
+    ("tall", 9000, 48, 64, 1),       # XCD shards: the other shards spin until spin_max
+])
+def test_xcd_misplacement_abort(monkeypatch, kind, m, ns, block, launch):
+    """a k_sel block that finds itself on another XCD than
+    its launch's others (injected: LPGPU_FAULT_XCC=<launch>) -- the launch is
+    abandoned (sel_flags 8) and redone on the per-pivot kernels, bit-exact"""
+    monkeypatch.setenv("LPGPU_FAULT_XCC", str(launch))
+    monkeypatch.setenv("LPGPU_SPIN_MAX", "20000")
+    monkeypatch.delenv("LPGPU_STRICT", raising=False)
+    T = gen.tableau(kind, m, ns, 19)
+    e = _engine(T, block)
+    k = 150
+    st, done = e.run(_lib.RULE_STANDARD, k)
+    o = F64Tableau(T)
+    ost, olog = o.run(0, k)
+    assert len(olog) > 64 * (launch - 1)              # the faulted launch ran
+    assert e.log().tolist() == olog.tolist()
+    assert _bits_equal(e.download(), o.T)
+    assert e.exchange_path() == (_lib.PATH_KERNELS, 1)
+    e.close()
+
+
+@pytest.mark.parametrize("kind,m,ns", [("mixed", 700, 900), ("tall", 17000, 70)])
+@pytest.mark.parametrize("block,ks", [(64, (70, 5, 1, 33, 121)), (50, (120, 7)), (57, (57, 114))])
+def test_partial_groups_padded_sweep(kind, m, ns, block, ks):
+    """groups shorter than 64 -- a run that ends inside
+    a group (64 + 57: the zero-padded k_sweep_rl pass; 64 + 6: k_sweep_dp2 at
+    16), depths of 49..63 (every group padded), explicit Tableau.pivot calls
+    (one pivot each) and findPivot*(True) -- every bit as the f64 oracle's"""
+    T = gen.tableau(kind, m, ns, 23)
+    e = _engine(T, block)
+    o = F64Tableau(T)
+    for k in ks:
+        st, done = e.run(_lib.RULE_STANDARD, k)
+        ost, olog = o.run(0, k)
+        assert done == len(olog)
+        assert _bits_equal(e.download(), o.T), k
+    assert e.exchange_path()[1] == 0
+    for _ in range(6):
+        want = o.find(0)
+        if isinstance(want, str):
+            break
+        e.pivot(*want)
+        o.pivot(*want)
+    assert _bits_equal(e.download(), o.T)
+    for _ in range(3):
+        got = e.find(_lib.RULE_STANDARD, True)
+        want = o.find(0)
+        assert (list(got) if isinstance(got, tuple) else got) == (list(want) if isinstance(want, tuple) else want)
+        if isinstance(want, str):
+            break
+        o.pivot(*want)
+    assert _bits_equal(e.download(), o.T)
+    e.close()
+
+
+def test_explicit_pivots_at_depth_64_cfg3():
+    """explicit pivots (one-pivot groups) on the cfg3 tableau at 64 pivots per
+    sweep: each is one pass of k_sweep_dp2 at depth 16 (the host knows the
+    group holds one pivot), not a per-element fallback; 20 pivots bit-exact"""
+    T = gen.tableau("mixed", 4096, 4096, 3)
+    e = _engine(T, 64)
+    o = F64Tableau(T)
+    seq = []
+    for _ in range(20):
+        p = o.find(0)
+        seq.append(p)
+        o.pivot(*p)
+    e.pivot(*seq[0])                                  # warm-up
+    t0 = time.perf_counter()
+    for p in seq[1:]:
+        e.pivot(*p)
+    dt = (time.perf_counter() - t0) / (len(seq) - 1)
+    print(f"explicit pivot at block 64 on cfg3: {dt * 1e3:.3f} ms per call")
+    assert _bits_equal(e.download(), o.T)
+    assert dt < 0.02, dt                              # a padded pass is ~0.15 ms of sweep + launches
+    e.close()
