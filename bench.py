@@ -56,6 +56,10 @@ TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r03", "hbm_traffic.json")
 WORKLOADS = {
     "cfg4": ("tall", 32768, 8192, "cfg4: 32768x8192 float64 tableau, G_tall seed 3"),
     "cfg3": ("mixed", 4096, 4096, "cfg3: 4096x8192 float64 tableau, G_mixed seed 3"),
+    # rehearsal of one rank of the 8-GPU cfg4 job (4096 rows per rank, the
+    # one-XCD cross-rank kernel k_sel<XR>, G = 64) with two ranks on ONE GPU:
+    # 6144 columns, so both ranks' launches are resident at once
+    "cfg4r8": ("tall", 8192, 6144, "8192x6144 G_tall seed 3: two 4096-row ranks (the 8-GPU cfg4 rank geometry)"),
 }
 
 
@@ -436,7 +440,7 @@ def main():
         assert (eng.row_begin, eng.row_count) == (rb, re_ - rb)
         if args.no_rccl:
             eng.set_host_allgather(_lib.gloo_allgather())
-        ok, why = 0, "not requested"
+        ok, why = 0, "not requested (--exchange rccl)"
         if args.exchange != "rccl" or args.no_rccl:
             try:
                 hs = [None] * world
@@ -444,12 +448,18 @@ def main():
                 eng.peer_open(b"".join(hs))
                 ok, why = 1, ""
             except (_lib.DeviceError, ValueError) as ex:
-                why = str(ex)
-        flag = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag[0]) != 1:
+                why = f"peer_open failed: {ex}"
+        # every rank's verdict on the device-side exchange (a job leaves the
+        # peer path if any rank could not open it: one line says which and why)
+        verdicts = [None] * world
+        dist.all_gather_object(verdicts, (rank, ok, why))
+        peer_fail = [(r, w) for r, o, w in verdicts if not o]
+        if peer_fail:
             if args.exchange == "peer":
-                raise SystemExit(f"peer exchange unavailable on some rank: {why}")
+                raise SystemExit(f"peer exchange unavailable: rank {peer_fail[0][0]}: {peer_fail[0][1]}")
+            if rank == 0:
+                print(f"bench: leaving the peer exchange (one RCCL collective per pivot instead): "
+                      f"rank {peer_fail[0][0]}: {peer_fail[0][1]}", file=sys.stderr, flush=True)
             if ok:
                 eng.peer_enable(False)
         eng.set_block(B)
@@ -466,10 +476,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, sw_ms, sel_ms, hop_us = float(t[0]), float(t[1]), float(t[2]), float(t[3])
         # distinct GPUs of the job (ranks wrap onto fewer GPUs on a small box)
-        ids = [None] * world
-        dist.all_gather_object(ids, (os.uname().nodename, device))
-        devices = len(set(ids))
+        # and the selection kernel every rank actually ran (its last launch)
         path, fallbacks = eng.exchange_path()
+        geo = eng.geometry()
+        kern = geo["kernel"] + (f" as {geo['xcd_shards']} XCD shards" if geo.get("xcd_shards") else
+                                " on one XCD" if geo.get("on_one_xcd") else "")
+        ids = [None] * world
+        dist.all_gather_object(ids, (os.uname().nodename, device, rank, kern, _lib.PATH_NAMES.get(path, path),
+                                     fallbacks))
+        devices = len(set((h, d) for h, d, *_ in ids))
         share = "" if devices == world else f", {world} ranks sharing {devices} GPU(s)"
         parallelism = (f"row-shard x{world} over {'xGMI' if devices == world else 'one GPU'}: "
                        f"{_lib.PATH_NAMES.get(path, path)}{share}")
@@ -477,8 +492,12 @@ def main():
         sweep_ms = sw_ms
         acc = accounting(args.steps, B, elapsed, sw_ms, sel_ms, local_rows, n)
         acc.update(fallbacks=fallbacks, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
-                   selection_avg_launch_us=sel_ms * 1e3, selection_kernel=eng.geometry()["kernel"],
-                   xrank_hop_us_per_pivot=hop_us)
+                   selection_avg_launch_us=sel_ms * 1e3, selection_kernel=kern,
+                   xrank_hop_us_per_pivot=hop_us,
+                   ranks=[{"rank": r, "host": h, "device": d, "selection_kernel": k, "path": pth, "fallbacks": fb}
+                          for h, d, r, k, pth, fb in ids],
+                   peer_exchange={"ok": not peer_fail,
+                                  "reason": (f"rank {peer_fail[0][0]}: {peer_fail[0][1]}" if peer_fail else "")})
         elapsed_pps = acc["pivots_per_s"]
 
     desc = WORKLOADS[args.workload][3]
@@ -537,6 +556,7 @@ def main():
             **({"xcd_hop_us_per_pivot": acc["xcd_hop_us_per_pivot"]} if "xcd_hop_us_per_pivot" in acc else {}),
         },
         "fallbacks": acc["fallbacks"],
+        **({"ranks": acc["ranks"], "peer_exchange": acc["peer_exchange"]} if world > 1 else {}),
         "src_sha256": digest,
         "lib_sha256": lib_digest(),
     })
