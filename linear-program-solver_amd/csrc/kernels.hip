@@ -2029,6 +2029,44 @@ __device__ __forceinline__ void lds_mult(double (&m)[NC], unsigned a)
     }
 }
 
+// k_sweep_rl's pivot-row fix-up: the batch row's multipliers of pivots
+// 8 H .. 8 H + 7 (one MQ quad: 32 bytes apart) from LDS, uniform addresses
+template <int H>
+__device__ __forceinline__ void lds_mrow8(double (&v)[8], unsigned a)
+{
+    asm volatile("ds_read_b64 %0, %8 offset:%9\n ds_read_b64 %1, %8 offset:%10\n ds_read_b64 %2, %8 offset:%11\n"
+                 "ds_read_b64 %3, %8 offset:%12\n ds_read_b64 %4, %8 offset:%13\n ds_read_b64 %5, %8 offset:%14\n"
+                 "ds_read_b64 %6, %8 offset:%15\n ds_read_b64 %7, %8 offset:%16\n s_waitcnt lgkmcnt(0)"
+                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3]), "=v"(v[4]), "=v"(v[5]), "=v"(v[6]), "=v"(v[7])
+                 : "v"(a), "n"(256 * H), "n"(256 * H + 32), "n"(256 * H + 64), "n"(256 * H + 96), "n"(256 * H + 128),
+                   "n"(256 * H + 160), "n"(256 * H + 192), "n"(256 * H + 224));
+}
+// y (pivot row s0, this lane's column) <- P[s0] with pivots s0 + 1 .. NB - 1
+// applied, their multipliers of that row read from LDS at a (+ 32 s bytes),
+// 8 at a time; chunks that end at or before s0 are skipped.  (A branch-free
+// form -- 32 multipliers per read, the pivots up to s0 masked to exact
+// no-ops -- measured 170 against 122 us per cfg3 launch: its registers cost
+// the main loop)
+template <int NB, int H = 0>
+__device__ __forceinline__ void fix_chain(double &y, const double (&p)[NB], unsigned a, int s0)
+{
+    if constexpr (H == 0) {
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+            if (s == s0) y = p[s];
+    }
+    if constexpr (H < NB / 8) {
+        if (8 * H + 7 > s0) {
+            double v[8];
+            lds_mrow8<H>(v, a);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (8 * H + j > s0) y = fma(-v[j], p[8 * H + j], y);
+        }
+        fix_chain<NB, H + 1>(y, p, a, s0);
+    }
+}
+
 template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
@@ -2044,7 +2082,16 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     constexpr int RW = 8;                        // rows per batch
     constexpr int NC = NB / 2;                   // multiplier registers (2 pivots x 8 rows each)
     constexpr int XS = W * RW * 64;              // doubles of a slot's rows (W waves x 8 rows x 64 columns)
-    constexpr int MS = 2 * 4 * BMAX;             // doubles of a slot's multipliers (two MQ quads)
+    // a slot's multipliers: two MQ quads, the second QP doubles further on.
+    // The multiplier registers of 16 lanes read rows 0-3 of quad 0 and rows
+    // 4-7 of quad 1 at the same offsets: 2 KB apart they share LDS banks (a
+    // 2-way conflict on every read, SQ_LDS_BANK_CONFLICT 43 % of the LDS
+    // cycles at cfg3); 16 doubles further on they do not.
+#ifndef SWEEP_QP
+#define SWEEP_QP 16
+#endif
+    constexpr int QP = (D * (XS + 2 * 4 * BMAX + SWEEP_QP) * 8 + 8 * NB <= 80 * 1024 || W > 4) ? SWEEP_QP : 0;
+    constexpr int MS = 2 * 4 * BMAX + QP;        // doubles of a slot's multipliers
     static_assert(NB % 2 == 0 && NB <= BMAX && D >= 2 && W >= 4, "k_sweep_rl");
     __shared__ __attribute__((aligned(16))) double xs[D][XS];
     __shared__ __attribute__((aligned(16))) double ms[D][MS];
@@ -2054,6 +2101,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
+    auto srow = [&](int s) -> long long { return sr[s]; };
     const int strip = (int)(blockIdx.x % (unsigned)nstrips);
     const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
     const long long r1 = min(rows, r0 + run);
@@ -2078,7 +2126,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         auto one = [&](long long row, long long c, bool ok) {
             double x = T[row * ld + c];
             for (int s = 0; s < nd; ++s) {
-                if (sr[s] == row) x = P[(long long)s * ld + c];        // the pivot row becomes P[s]
+                if (srow(s) == row) x = P[(long long)s * ld + c];      // the pivot row becomes P[s]
                 else x = fma(-M[mq(row, s)], P[(long long)s * ld + c], x);
             }
             if (ok) Tout[row * ld + c] = x;
@@ -2090,14 +2138,16 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     double p[NB];
 #pragma unroll
     for (int s = 0; s < NB; ++s) p[s] = P[(long long)s * ld + col];
+    // lane s: pivot s's local row (-2: none / another rank's), for the
+    // batches that hold a pivot row of the group
+    const long long mysr = lane < nd ? dR[lane] : -2;
     const long long nbat = (r1 - r0 + RW - 1) / RW;
     const long long nquad = (rows + 3) >> 2;
     // copies of batch i into slot i % D: lane l of a wave brings 16 bytes --
     // rows: row 2 q + (l >> 5) of the wave's 8, columns 2 (l & 31) .. +1 of
     // its 64, for q = 0..3 (4 instructions); multipliers: quad (wave >> 1) of
     // the batch, bytes 1 KB x (wave & 1) + 16 l of it (one instruction)
-    auto issue = [&](long long i) {
-        const int slot = (int)(i % D);
+    auto issue = [&](long long i, int slot) {
         const long long rb = r0 + i * RW;
         const long long last = r1 - 1;
 #pragma unroll
@@ -2112,7 +2162,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         const int w4 = wave & 3;
         const long long qd = min((rb >> 2) + (w4 >> 1), nquad - 1);
         __builtin_amdgcn_global_load_lds(M + qd * (4 * BMAX) + (w4 & 1) * 128 + 2 * lane,
-                                         (__attribute__((address_space(3))) void *)&ms[slot][(w4 >> 1) * (4 * BMAX) + (w4 & 1) * 128],
+                                         (__attribute__((address_space(3))) void *)&ms[slot][(w4 >> 1) * (4 * BMAX + QP) + (w4 & 1) * 128],
                                          16, 0, 0);
     };
     // vector-memory instructions a wave issues per batch after the copies of
@@ -2120,7 +2170,8 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     constexpr int PER = 5 + RW;
     __syncthreads();                             // sr staged
 #pragma unroll 1
-    for (long long i = 0; i < D - 1; ++i) issue(i);
+    for (int i = 0; i < D - 1; ++i) issue(i, i);
+    int slot = 0;                                // batch i's slot, i % D
     const int vh = (lane & 15) >> 3, vk = lane & 7;
 #pragma unroll 1
     for (long long i = 0; i < nbat; ++i) {
@@ -2142,8 +2193,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");   // D == 4, i == 2
         }
         __syncthreads();                         // every wave's copies of batch i are in LDS
-        const int slot = (int)(i % D);
-        issue(min(i + D - 1, nbat - 1));         // into the slot batch i - 1 used (all waves past it)
+        issue(min(i + D - 1, nbat - 1), slot == 0 ? D - 1 : slot - 1);   // the slot batch i - 1 used
         const long long rb = r0 + i * RW;
         const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
         double x[RW], m[NC];
@@ -2154,7 +2204,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             // write made it wait for every copy in flight (vmcnt(0)) first;
             // the wait above already covers this batch's
             const unsigned xa = lds_off(&xs[slot][wave * RW * 64 + lane]);
-            const unsigned ma = lds_off(&ms[slot][(kr >> 2) * (4 * BMAX) + (kr & 3) + vh * 4]);
+            const unsigned ma = lds_off(&ms[slot][(kr >> 2) * (4 * BMAX + QP) + (kr & 3) + vh * 4]);
             lds_rows<RW>(x, xa);
             lds_mult<NC>(m, ma);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2167,12 +2217,27 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         } else {
 #pragma unroll
             for (int k = 0; k < RW; ++k) x[k] = xs[slot][(wave * RW + min(k, kmax)) * 64 + lane];
-            const double *mrow = &ms[slot][(kr >> 2) * (4 * BMAX) + (kr & 3)];
+            const double *mrow = &ms[slot][(kr >> 2) * (4 * BMAX + QP) + (kr & 3)];
 #pragma unroll
             for (int c = 0; c < NC; ++c) m[c] = mrow[(2 * c + vh) * 4];
         }
 #pragma unroll
         for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
+        // a pivot row s0 of the group in this batch (about one batch in eight
+        // at cfg3): it holds P[s0] after pivot s0 and takes only the later
+        // pivots -- recomputed here from P (registers) and its multipliers
+        // (this batch's LDS slot), not re-read from memory after the pass
+        for (u64 hit = __ballot(mysr >= rb && mysr <= rb + kmax); hit; hit &= hit - 1) {
+            const int s0 = __builtin_ctzll(hit);
+            const int k = (int)(__builtin_amdgcn_readlane((int)(unsigned)mysr, s0) - (int)(unsigned)rb);
+            double y = 0.0;
+            fix_chain<NB>(y, p, lds_off(&ms[slot][(k >> 2) * (4 * BMAX + QP) + (k & 3)]), s0);
+            // (a last, partial batch stores row kmax from every x[k >= kmax]:
+            // all of them take the fixed value)
+#pragma unroll
+            for (int kk = 0; kk < RW; ++kk)
+                if (min(kk, kmax) == k) x[kk] = y;
+        }
         {
             // write-through stores (SA), as the DPP sweeps'.  A wave whose 64
             // columns lie past the pitch (ld is a multiple of 64, so a wave is
@@ -2187,22 +2252,13 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             for (int k = 0; k < RW; ++k)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, x[k]), ro, voff, min(k, kmax) * ldb, SA);
         }
+        slot = slot + 1 == D ? 0 : slot + 1;
     }
-    // the group's pivot rows in this run: recomputed after the pass (rare)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int s0 = 0; s0 < nd; ++s0) {
-        const long long row = sr[s0];
-        if (row < r0 || row >= r1) continue;     // block-uniform
-        double y = p[0];
-#pragma unroll
-        for (int s = 0; s < NB; ++s)
-            if (s == s0) y = p[s];
-#pragma unroll
-        for (int s = 0; s < NB; ++s)
-            if (s > s0) y = fma(-M[mq(row, s)], p[s], y);
-        if (cok) Tout[row * ld + col] = y;
-    }
+#ifdef SWEEP_PROBE_NO_EPI
+    if (nd > 0) return;                          // timing probe only: results NOT kept
+#endif
     if (t0 >= t1) return;                        // block-uniform: no tail piece
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ---- the tail piece: the 64 columns from tcol (one per lane) of rows
     //      [t0, t1), wave w on batches t0 + 8 w, t0 + 8 (w + W), ...: the same
     //      register FMAs with every operand loaded from memory (a few batches
@@ -2226,7 +2282,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int s0 = 0; s0 < nd; ++s0) {
-        const long long row = sr[s0];
+        const long long row = srow(s0);
         if (row < t0 || row >= t1 || (row - t0) / RW % W != wave) continue;   // the wave that stored it
         double y = p[0];
 #pragma unroll
@@ -2534,7 +2590,12 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         // faster than 3 deep).  W = 8 waves for long runs (cfg4: 904 against
         // 930 us at W = 4), 4 for short ones (cfg3: 141 against 149 us)
         constexpr int DL = 2;
-        const bool w8 = A.rows >= 16384;
+        static int w8_env = -1;
+        if (w8_env < 0) {
+            const char *v = std::getenv("LPGPU_SWEEP_W8");   // A/B: 1 = 8 waves at any height
+            w8_env = v ? std::atoi(v) : 0;
+        }
+        const bool w8 = A.rows >= 16384 || w8_env == 1;
         const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
 #define RL_FN(WV) (nb == 16 ? (const void *)&k_sweep_rl<WV, 16, DL, SA>   \
                  : nb == 32 ? (const void *)&k_sweep_rl<WV, 32, DL, SA> \

@@ -1,0 +1,6 @@
+source scripts/r4_call.sh
+VD=$PWD/linear-program-solver_amd/lpsol_amd/_lib/variants
+step t 900 gpurun_out/t9.log python -u -m pytest -q --timeout 600 --timeout-method thread tests/test_gpu_r4.py tests/test_gpu_r3.py tests/test_gpu_parity.py
+step ab3 600 gpurun_out/ab3.log bash scripts/ab_env.sh cfg3 2 - LPGPU_LIB=$VD/noepi.so
+step ab4 900 gpurun_out/ab4.log bash scripts/ab_env.sh cfg4 2 - LPGPU_LIB=$VD/noepi.so
+source scripts/c8.sh
