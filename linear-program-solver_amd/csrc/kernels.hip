@@ -2067,6 +2067,88 @@ __device__ __forceinline__ void fix_chain(double &y, const double (&p)[NB], unsi
     }
 }
 
+// pivots 16 K + j0 .. 16 K + j1 - 1 of a pivot-row chain: y <- fma(-m[lane
+// 16 K + j of the 16-lane row], p[16 K + j], y), the multiplier broadcast by
+// DPP (lane l of mk holds pivot 16 K + (l & 15)'s multiplier of the row)
+template <int J>
+__device__ __forceinline__ void fix1(double &y, double mk, double pj)
+{
+    asm("s_nop 4\n v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(y)
+        : "v"(mk), "v"(pj), "n"(J));
+}
+#define FXF(L, P) "v_fmac_f64_dpp %0, -%1, %" #P " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
+template <int K, int NB>
+__device__ __forceinline__ void fix16(double &y, double mk, const double (&p)[NB])
+{
+    asm("s_nop 4\n" FXF(0, 2) FXF(1, 3) FXF(2, 4) FXF(3, 5) FXF(4, 6) FXF(5, 7) FXF(6, 8) FXF(7, 9) FXF(8, 10)
+            FXF(9, 11) FXF(10, 12) FXF(11, 13) FXF(12, 14) FXF(13, 15) FXF(14, 16) FXF(15, 17)
+        : "+v"(y)
+        : "v"(mk), "v"(p[16 * K]), "v"(p[16 * K + 1]), "v"(p[16 * K + 2]), "v"(p[16 * K + 3]),
+          "v"(p[16 * K + 4]), "v"(p[16 * K + 5]), "v"(p[16 * K + 6]), "v"(p[16 * K + 7]), "v"(p[16 * K + 8]),
+          "v"(p[16 * K + 9]), "v"(p[16 * K + 10]), "v"(p[16 * K + 11]), "v"(p[16 * K + 12]),
+          "v"(p[16 * K + 13]), "v"(p[16 * K + 14]), "v"(p[16 * K + 15]));
+}
+#undef FXF
+template <int K, int NB, int J = 0>
+__device__ __forceinline__ void fix16_after(double &y, double mk, const double (&p)[NB], int s0)
+{
+    if constexpr (J < 16) {
+        if (16 * K + J > s0) fix1<J>(y, mk, p[16 * K + J]);      // uniform
+        fix16_after<K, NB, J + 1>(y, mk, p, s0);
+    }
+}
+template <int NB, int K = 0>
+__device__ __forceinline__ void fix_chain_dpp(double &y, const double (&mk)[NB / 16], const double (&p)[NB], int s0)
+{
+    if constexpr (K < NB / 16) {
+        if (16 * K > s0) fix16<K, NB>(y, mk[K], p);            // uniform: every pivot after s0
+        else if (16 * K + 15 > s0) fix16_after<K, NB>(y, mk[K], p, s0);
+        fix_chain_dpp<NB, K + 1>(y, mk, p, s0);
+    }
+}
+// The group's pivot rows among local rows [ra, rz), on this lane's column
+// col: a pivot row s0 holds P[s0] after pivot s0 and takes only the later
+// pivots (upd()).  Rewritten after the pass (every store of the pass has
+// landed: vmcnt(0) before), two rows per round trip: lane l loads the row's
+// multipliers of pivots 16 k + (l & 15), k = 0..3 (MQ), and P[s0] at its
+// column; then each row's chain runs from registers with the multiplier
+// broadcast by DPP.  (fmod > 0: only the rows of the 8-row batches fsel,
+// fsel + fmod, ... from ra -- the tail piece's batches of one wave)
+template <int NB>
+__device__ __forceinline__ void fix_rows(const double *__restrict__ P, const double *__restrict__ M,
+                                         double *Tout, long long ld, long long col, bool ok,
+                                         const double (&p)[NB], long long mysr, long long ra, long long rz,
+                                         int fmod = 0, int fsel = 0)
+{
+    static_assert(NB % 16 == 0, "fix_rows: pivots in 16s");
+    constexpr int NK = NB / 16;
+    const int lane = threadIdx.x & 63;
+    u64 h = __ballot(mysr >= ra && mysr < rz && (fmod == 0 || (int)((mysr - ra) >> 3) % fmod == fsel));
+    while (h) {
+        const int sa = __builtin_ctzll(h);
+        h &= h - 1;
+        const bool two = h != 0;
+        const int sb = two ? __builtin_ctzll(h) : sa;
+        if (two) h &= h - 1;
+        const long long ra_ = (long long)__builtin_amdgcn_readlane((int)(unsigned)mysr, sa);
+        const long long rb_ = (long long)__builtin_amdgcn_readlane((int)(unsigned)mysr, sb);
+        double ma[NK], mb[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            ma[k] = M[mq(ra_, 16 * k + (lane & 15))];
+            mb[k] = M[mq(rb_, 16 * k + (lane & 15))];
+        }
+        double ya = P[(long long)sa * ld + col], yb = P[(long long)sb * ld + col];
+        fix_chain_dpp<NB>(ya, ma, p, sa);
+        if (ok) Tout[ra_ * ld + col] = ya;
+        if (two) {
+            fix_chain_dpp<NB>(yb, mb, p, sb);
+            if (ok) Tout[rb_ * ld + col] = yb;
+        }
+    }
+}
+
 template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
@@ -2227,6 +2309,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         // at cfg3): it holds P[s0] after pivot s0 and takes only the later
         // pivots -- recomputed here from P (registers) and its multipliers
         // (this batch's LDS slot), not re-read from memory after the pass
+#ifdef SWEEP_FIX_INLOOP
         for (u64 hit = __ballot(mysr >= rb && mysr <= rb + kmax); hit; hit &= hit - 1) {
             const int s0 = __builtin_ctzll(hit);
             const int k = (int)(__builtin_amdgcn_readlane((int)(unsigned)mysr, s0) - (int)(unsigned)rb);
@@ -2238,6 +2321,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             for (int kk = 0; kk < RW; ++kk)
                 if (min(kk, kmax) == k) x[kk] = y;
         }
+#endif
         {
             // write-through stores (SA), as the DPP sweeps'.  A wave whose 64
             // columns lie past the pitch (ld is a multiple of 64, so a wave is
@@ -2255,6 +2339,14 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         slot = slot + 1 == D ? 0 : slot + 1;
     }
 #ifdef SWEEP_PROBE_NO_EPI
+    if (nd > 0) return;                          // timing probe only: results NOT kept
+#endif
+#ifndef SWEEP_FIX_INLOOP
+    // the group's pivot rows in this run: every store of the pass has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fix_rows<NB>(P, M, Tout, ld, col, cok, p, mysr, r0, r1);
+#endif
+#ifdef SWEEP_PROBE_NO_TAIL
     if (nd > 0) return;                          // timing probe only: results NOT kept
 #endif
     if (t0 >= t1) return;                        // block-uniform: no tail piece
@@ -2280,19 +2372,10 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             for (int k = 0; k < RW; ++k) Tout[(rb + min(k, kmax)) * ld + tc] = x[k];
         }
     }
+    // the tail's pivot rows, by the wave that stored them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (int s0 = 0; s0 < nd; ++s0) {
-        const long long row = srow(s0);
-        if (row < t0 || row >= t1 || (row - t0) / RW % W != wave) continue;   // the wave that stored it
-        double y = p[0];
-#pragma unroll
-        for (int s = 0; s < NB; ++s)
-            if (s == s0) y = p[s];
-#pragma unroll
-        for (int s = 0; s < NB; ++s)
-            if (s > s0) y = fma(-M[mq(row, s)], p[s], y);
-        if (tok) Tout[row * ld + tc] = y;
-    }
+    static_assert(RW == 8, "fix_rows: 8-row batches");
+    fix_rows<NB>(P, M, Tout, ld, tc, tok, p, mysr, t0, t1, W, wave);
 }
 
 // peer exchange check (row-sharded setup): lane p writes this rank's granule
