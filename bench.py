@@ -21,7 +21,12 @@ replicated).  At N = 1 the line also carries ``cfg3``: the 4096 x 8192
 G_mixed tableau (config 3, the north star's 60 %-of-HBM-roofline case)
 measured the same way.  ``--workload cfg3`` makes cfg3 the main workload.
 
-Inputs are resident in HBM before the timed region.  Every 8th sweep and
+Inputs are resident in HBM before the timed region.  Before the W warmup
+steps, a device warm-up (``--device-warmup-ms``, 150 ms) runs the same
+workload's groups on a SCRATCH copy of the tableau: after the idle gap of the
+upload the MI355X runs the sweep 10-15 % slower for ~30 launches whatever the
+data (scripts/ramp_probe2.py); the benchmarked engine still starts its warmup
+steps from the initial tableau.  Every 8th sweep and
 selection launch inside the timed region records a pair of HIP events at the
 kernel's start and end (hipExtLaunchKernelGGL on the engine's stream); the
 roofline's achieved bandwidth is the sweep's algorithmic bytes over that
@@ -287,12 +292,41 @@ def config_table(cpu_budget: float = 20.0) -> None:
         }), flush=True)
 
 
-def upload(engines, kind, m, ns, spans, blk=2048):
-    """rows of the workload into each engine (row 0 + its row block)"""
-    for e, (a0, a1) in zip(engines, spans):
-        e.put_rows(0, gen.rows(kind, m, ns, SEED, 0, 1))
+def upload(engines, kind, m, ns, spans, blk=2048, heaters=None):
+    """rows of the workload into each engine (row 0 + its row block); a
+    heater engine beside one (device_warmup) gets the same rows, locally
+    numbered"""
+    heaters = heaters or [None] * len(engines)
+    for e, h, (a0, a1) in zip(engines, heaters, spans):
+        R = gen.rows(kind, m, ns, SEED, 0, 1)
+        e.put_rows(0, R)
+        if h is not None:
+            h.put_rows(0, R)
         for a in range(a0, a1, blk):
-            e.put_rows(1 + a, gen.rows(kind, m, ns, SEED, 1 + a, 1 + min(a + blk, a1)))
+            R = gen.rows(kind, m, ns, SEED, 1 + a, 1 + min(a + blk, a1))
+            e.put_rows(1 + a, R)
+            if h is not None:
+                h.put_rows(1 + a - a0, R)
+
+
+def device_warmup(heater, block: int, ms: float) -> dict:
+    """Keep the GPU busy for `ms` right before the warmup steps: groups of
+    the same workload on a SCRATCH copy of the rank's tableau (`heater`), so
+    the benchmarked engine still starts its W warmup steps from the initial
+    tableau.  Why: after an idle gap (the upload) the MI355X runs the sweep
+    10-15 % slower for its first ~30 launches, whatever the data -- the same
+    tableau re-uploaded ramps again, the initial tableau right after another
+    engine's groups does not (scripts/ramp_probe2.py, profiles/r04/README.md)."""
+    if heater is None or ms <= 0:
+        return {"ms": 0.0, "groups": 0}
+    t0 = time.perf_counter()
+    groups = 0
+    while (time.perf_counter() - t0) * 1e3 < ms and groups < 4096:
+        st, done = heater.run(_lib.RULE_STANDARD, 8 * block)
+        groups += done // block
+        if done < 8 * block:
+            break                                # the scratch LP ended: warm enough or not, stop
+    return {"ms": (time.perf_counter() - t0) * 1e3, "groups": groups}
 
 
 def accounting(steps: int, block: int, elapsed: float, sweep_avg_ms: float, sel_avg_ms: float,
@@ -317,9 +351,12 @@ def accounting(steps: int, block: int, elapsed: float, sweep_avg_ms: float, sel_
     }
 
 
-def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int):
-    """warmup groups, then exactly `steps` timed groups bracketed by the
-    barrier + stream sync (lp_run ends with a stream sync)."""
+def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int, heater=None, heat_ms: float = 0.0):
+    """device warm-up on the heater (untimed, another tableau), warmup groups,
+    then exactly `steps` timed groups bracketed by the barrier + stream sync
+    (lp_run ends with a stream sync)."""
+    heat = device_warmup(heater, block, heat_ms)
+    barrier()                                    # ranks enter the warmup together (the exchange needs all)
     st, done = eng.run(_lib.RULE_STANDARD, warmup * block)
     if done != warmup * block:
         raise SystemExit(f"warmup ended early: status {st} after {done} pivots")
@@ -335,11 +372,11 @@ def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int):
     upd_ms, upd_n = eng.update_time()
     sel_ms, sel_n = eng.select_time()
     eng.profile(False)
-    return t1 - t0, upd_ms / max(upd_n, 1), (sel_ms / sel_n if sel_n else 0.0), upd_n, sel_n
+    return t1 - t0, upd_ms / max(upd_n, 1), (sel_ms / sel_n if sel_n else 0.0), upd_n, sel_n, heat
 
 
 def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, device: int,
-                   shards: int = 0) -> dict:
+                   shards: int = 0, heat_ms: float = 0.0) -> dict:
     """one workload on one GPU (or as `shards` in-process row shards of it,
     a diagnostic): timing, roofline and selection figures"""
     kind, m, ns, n, _, _ = workload(name, 1, 0)
@@ -352,9 +389,16 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
     for e in engs:
         e.set_block(block)
     block = engs[0].get_block()          # the auto choice (--block 0) resolved
-    upload(engs, kind, m, ns, spans)
+    heater = None
+    if heat_ms > 0 and not shards:
+        heater = _lib.Engine(m, n, device=device)
+        heater.set_block(block)
+    upload(engs, kind, m, ns, spans, heaters=[heater] if heater else None)
     xw0 = engs[0].xwait()
-    elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(engs[0], steps, warmup, block, lambda: None, every)
+    elapsed, sw_ms, sel_ms, sw_n, sel_n, heat = timed_run(engs[0], steps, warmup, block, lambda: None, every,
+                                                          heater, heat_ms)
+    if heater is not None:
+        heater.close()
     xw1 = engs[0].xwait()
     path, fallbacks = engs[0].exchange_path()
     geo = engs[0].geometry()
@@ -366,7 +410,7 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
         acc["selection_kernel"] += f" as {geo['xcd_shards']} XCD row shards"
         acc["xcd_hop_us_per_pivot"] = (1e6 * (xw1[0] - xw0[0]) / (xw1[1] - xw0[1])
                                        if xw1[1] > xw0[1] else 0.0)
-    acc.update(block=block, path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks,
+    acc.update(block=block, path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks, device_warmup=heat,
                sweep_avg_us=sw_ms * 1e3, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
                selection_avg_launch_us=sel_ms * 1e3)
     for e in reversed(engs):
@@ -398,6 +442,9 @@ def main():
                     help="1-GPU diagnostic: the workload as S in-process row shards on one GPU")
     ap.add_argument("--profile-every", type=int, default=8,
                     help="time every k-th launch of each kernel with HIP events (1 = all)")
+    ap.add_argument("--device-warmup-ms", type=float, default=150.0,
+                    help="before the W warmup steps, keep the GPU busy this long with the same "
+                         "workload on a scratch copy of the tableau (0: off; see device_warmup)")
     ap.add_argument("--configs", action="store_true",
                     help="instead of the benchmark: cfg1/cfg2/cfg5 on GPU 0 next to the "
                          "exact-Fraction CPU path, one JSON line each")
@@ -423,7 +470,7 @@ def main():
 
     if world == 1:
         leg = single_gpu_leg(args.workload, args.steps, args.warmup, B, args.profile_every, device,
-                             args.group_shards)
+                             args.group_shards, args.device_warmup_ms)
         elapsed_pps, devices = leg["pivots_per_s"], 1
         parallelism = (f"1 GPU ({leg['path']})" if not args.group_shards else
                        f"diagnostic: {args.group_shards} in-process row shards on 1 GPU ({leg['path']})")
@@ -464,10 +511,23 @@ def main():
                 eng.peer_enable(False)
         eng.set_block(B)
         B = eng.get_block()
-        upload([eng], kind, m, ns, [(rb, re_)])
+        # the device warm-up: the rank's rows as a plain one-GPU tableau (no
+        # exchange; load only) -- only when every rank has a GPU of its own
+        # (co-located ranks' persistent selections would contend for one XCD)
+        gpus = [None] * world
+        dist.all_gather_object(gpus, (os.uname().nodename, device))
+        heater = None
+        if args.device_warmup_ms > 0 and len(set(gpus)) == world:
+            heater = _lib.Engine(re_ - rb, n, device=device)
+            heater.set_block(B)
+        upload([eng], kind, m, ns, [(rb, re_)], heaters=[heater])
         xw0 = eng.xwait()
-        elapsed, sw_ms, sel_ms, sw_n, sel_n = timed_run(eng, args.steps, args.warmup, B,
-                                                        dist.barrier, args.profile_every)
+        elapsed, sw_ms, sel_ms, sw_n, sel_n, heat = timed_run(eng, args.steps, args.warmup, B, dist.barrier,
+                                                              args.profile_every, heater, args.device_warmup_ms)
+        if heater is not None:
+            heater.close()
+        elif args.device_warmup_ms > 0:
+            heat["skipped"] = "ranks share a GPU"
         xw1 = eng.xwait()
         # the cross-rank hop per pivot (block 0: its summary sent -> the
         # winner's pivot row held), over the timed pivots
@@ -491,7 +551,7 @@ def main():
         local_rows = (re_ - rb) + 1          # the largest block: ranks differ by <= 1 row
         sweep_ms = sw_ms
         acc = accounting(args.steps, B, elapsed, sw_ms, sel_ms, local_rows, n)
-        acc.update(fallbacks=fallbacks, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
+        acc.update(fallbacks=fallbacks, sweep_launches_timed=sw_n, selection_launches_timed=sel_n, device_warmup=heat,
                    selection_avg_launch_us=sel_ms * 1e3, selection_kernel=kern,
                    xrank_hop_us_per_pivot=hop_us,
                    ranks=[{"rank": r, "host": h, "device": d, "selection_kernel": k, "path": pth, "fallbacks": fb}
@@ -556,12 +616,16 @@ def main():
             **({"xcd_hop_us_per_pivot": acc["xcd_hop_us_per_pivot"]} if "xcd_hop_us_per_pivot" in acc else {}),
         },
         "fallbacks": acc["fallbacks"],
+        # untimed, before the W warmup steps: the same workload's groups on a
+        # scratch copy of the tableau (device_warmup; --device-warmup-ms 0: off)
+        "device_warmup": {**acc["device_warmup"], "on": "scratch copy of the workload's tableau"},
         **({"ranks": acc["ranks"], "peer_exchange": acc["peer_exchange"]} if world > 1 else {}),
         "src_sha256": digest,
         "lib_sha256": lib_digest(),
     })
     if world == 1 and args.workload != "cfg3" and not args.no_cfg3 and not args.group_shards:
-        c3 = single_gpu_leg("cfg3", args.steps, args.warmup, args.block, args.profile_every, device)
+        c3 = single_gpu_leg("cfg3", args.steps, args.warmup, args.block, args.profile_every, device,
+                            heat_ms=args.device_warmup_ms)
         out["cfg3"] = {
             "workload": WORKLOADS["cfg3"][3], "value": c3["pivots_per_s"], "unit": "pivots/s",
             "ms_per_step": c3["ms_per_step"], "us_per_pivot": 1e6 / c3["pivots_per_s"],

@@ -2003,6 +2003,10 @@ __device__ __forceinline__ unsigned lds_off(const double *p)
 {
     return (unsigned)(unsigned long)(const __attribute__((address_space(3))) double *)p;
 }
+__device__ __forceinline__ unsigned lds_off(const int *p)
+{
+    return (unsigned)(unsigned long)(const __attribute__((address_space(3))) int *)p;
+}
 // k_sweep_rl's rows: x[k] = LDS[a + 512 k]
 template <int RW>
 __device__ __forceinline__ void lds_rows(double (&x)[RW], unsigned a)
@@ -2115,24 +2119,65 @@ __device__ __forceinline__ void fix_chain_dpp(double &y, const double (&mk)[NB /
 // column; then each row's chain runs from registers with the multiplier
 // broadcast by DPP.  (fmod > 0: only the rows of the 8-row batches fsel,
 // fsel + fmod, ... from ra -- the tail piece's batches of one wave)
+// the next pivot row of the lanes h (the lowest lane's row) and the LAST
+// pivot of the group on that row (a row pivoted twice in the group ends as
+// the later pivot's row plus the pivots after it: the earlier chain is
+// dead); clears every lane of that row from h
+__device__ __forceinline__ int next_pivot_row(u64 &h, long long mysr, int &row)
+{
+    row = __builtin_amdgcn_readlane((int)(unsigned)mysr, __builtin_ctzll(h));
+    const u64 same = __ballot((int)(unsigned)mysr == row) & h;
+    h &= ~same;
+    return 63 - __builtin_clzll(same);
+}
+// p[s0] for a wave-uniform s0: a tree of uniform branches (no per-element
+// selects)
+template <int L, int N, int NB>
+__device__ __forceinline__ double pick_p(const double (&p)[NB], int s0)
+{
+    if constexpr (N == 1) {
+        double v = p[L];
+        asm volatile("" : "+v"(v));              // opaque: no select-of-loads fold (p to scratch)
+        return v;
+    } else {
+        if (s0 < L + N / 2) return pick_p<L, N / 2, NB>(p, s0);
+        return pick_p<L + N / 2, N - N / 2, NB>(p, s0);
+    }
+}
+// LDS moves written in asm (k_sweep_rl: a compiler-visible LDS access makes
+// the compiler wait for every LDS-DMA copy in flight first)
+__device__ __forceinline__ double lds_ld64(unsigned a)
+{
+    double v;
+    asm volatile("ds_read_b64 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_st64(unsigned a, double v)
+{
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st32(unsigned a, int v)
+{
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
 template <int NB>
 __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const double *__restrict__ M,
                                          double *Tout, long long ld, long long col, bool ok,
                                          const double (&p)[NB], long long mysr, long long ra, long long rz,
-                                         int fmod = 0, int fsel = 0)
+                                         int fmod = 0, int fsel = 0, u64 only = ~0ull)
 {
     static_assert(NB % 16 == 0, "fix_rows: pivots in 16s");
     constexpr int NK = NB / 16;
     const int lane = threadIdx.x & 63;
-    u64 h = __ballot(mysr >= ra && mysr < rz && (fmod == 0 || (int)((mysr - ra) >> 3) % fmod == fsel));
+    u64 h = __ballot(mysr >= ra && mysr < rz && (fmod == 0 || (int)((mysr - ra) >> 3) % fmod == fsel)) & only;
     while (h) {
-        const int sa = __builtin_ctzll(h);
-        h &= h - 1;
+        int ra32, rb32;
+        const int sa = next_pivot_row(h, mysr, ra32);
         const bool two = h != 0;
-        const int sb = two ? __builtin_ctzll(h) : sa;
-        if (two) h &= h - 1;
-        const long long ra_ = (long long)__builtin_amdgcn_readlane((int)(unsigned)mysr, sa);
-        const long long rb_ = (long long)__builtin_amdgcn_readlane((int)(unsigned)mysr, sb);
+        const int sb = two ? next_pivot_row(h, mysr, rb32) : sa;
+        if (!two) rb32 = ra32;
+        const long long ra_ = ra32, rb_ = rb32;
         double ma[NK], mb[NK];
 #pragma unroll
         for (int k = 0; k < NK; ++k) {
@@ -2178,6 +2223,15 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     __shared__ __attribute__((aligned(16))) double xs[D][XS];
     __shared__ __attribute__((aligned(16))) double ms[D][MS];
     __shared__ long long sr[NB];
+    // the group's pivot rows met in the pass: their multipliers (pivot l at
+    // [f][l]) copied out of the batch's slot, and (local row << 8 | last
+    // pivot on it), for the fix-up after the pass -- NF rows: 64 where the
+    // LDS allows (4-wave, 2 deep: 2 workgroups per CU still fit), else 16
+    // (the rest re-read from memory)
+    constexpr int LDS_BASE = D * (XS + MS) * 8 + NB * 8;
+    constexpr int NF = (W <= 4 && LDS_BASE + 64 * (NB * 8 + 4) <= 80 * 1024) ? 64 : 16;
+    __shared__ __attribute__((aligned(16))) double fixm[NF][NB];
+    __shared__ int fmeta[NF];
     const int nd = (int)ctl->ndef[grp];
     if (nd == 0 || ctl->bar_timeout) return;     // nothing deferred / group redone by the host
     const int lane = threadIdx.x & 63;
@@ -2220,9 +2274,6 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     double p[NB];
 #pragma unroll
     for (int s = 0; s < NB; ++s) p[s] = P[(long long)s * ld + col];
-    // lane s: pivot s's local row (-2: none / another rank's), for the
-    // batches that hold a pivot row of the group
-    const long long mysr = lane < nd ? dR[lane] : -2;
     const long long nbat = (r1 - r0 + RW - 1) / RW;
     const long long nquad = (rows + 3) >> 2;
     // copies of batch i into slot i % D: lane l of a wave brings 16 bytes --
@@ -2251,10 +2302,22 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     // batch i: the copies of the next batches (5 each) and the stores (8 each)
     constexpr int PER = 5 + RW;
     __syncthreads();                             // sr staged
+    // lane s: pivot s's local row (-2: none / another rank's).  From LDS,
+    // before the first copies: a VGPR loaded from global memory and read in
+    // the pass made the compiler wait vmcnt(0) at the pass's barrier
+    const long long mysr = lane < NB ? sr[lane] : -2;
+    const u64 runpiv = __ballot(mysr >= r0 && mysr < r1);     // the run holds a pivot row
 #pragma unroll 1
     for (int i = 0; i < D - 1; ++i) issue(i, i);
+    // P's registers read here, after the first copies: the compiler's wait
+    // for their loads (vmcnt of the copies issued since) lands before the
+    // pass, not at a barrier inside it (a vmcnt(0) every batch otherwise)
+#pragma unroll
+    for (int s = 0; s < NB; ++s) asm volatile("" ::"v"(p[s]));
     int slot = 0;                                // batch i's slot, i % D
     const int vh = (lane & 15) >> 3, vk = lane & 7;
+    int nf = 0;                                  // pivot rows captured (wave-uniform)
+    u64 ovf = 0;                                 // pivot lanes past NF captured rows
 #pragma unroll 1
     for (long long i = 0; i < nbat; ++i) {
         // batch i's copies are the oldest outstanding but for the D - 2 later
@@ -2322,6 +2385,28 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
                 if (min(kk, kmax) == k) x[kk] = y;
         }
 #endif
+#ifndef SWEEP_FIX_INLOOP
+        // the group's pivot rows in this batch (about one batch in five at
+        // cfg3, one in sixty at cfg4): their multipliers, in this slot until
+        // the next iteration's copies, set aside in fixm -- one wave per row,
+        // lane l pivot l's -- so the fix-up after the pass needs no memory
+        // round trip
+        for (u64 hit = runpiv ? __ballot(mysr >= rb && mysr <= rb + kmax) : 0; hit;) {
+            int row;
+            const int sl = next_pivot_row(hit, mysr, row);
+            if (nf < NF) {
+                if (wave == nf % W) {
+                    const int k = row - (int)rb;
+                    const double v = lds_ld64(lds_off(&ms[slot][(k >> 2) * (4 * BMAX + QP) + (k & 3) + 4 * lane]));
+                    lds_st64(lds_off(&fixm[nf][lane]), v);
+                    if (lane == 0) lds_st32(lds_off(&fmeta[nf]), ((row - (int)r0) << 8) | sl);
+                }
+                ++nf;
+            } else {
+                ovf |= __ballot((int)(unsigned)mysr == row);
+            }
+        }
+#endif
         {
             // write-through stores (SA), as the DPP sweeps'.  A wave whose 64
             // columns lie past the pitch (ld is a multiple of 64, so a wave is
@@ -2342,9 +2427,25 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     if (nd > 0) return;                          // timing probe only: results NOT kept
 #endif
 #ifndef SWEEP_FIX_INLOOP
-    // the group's pivot rows in this run: every store of the pass has landed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    fix_rows<NB>(P, M, Tout, ld, col, cok, p, mysr, r0, r1);
+    // the group's pivot rows in this run, rewritten from registers and LDS
+    // (pivot row s0: P[s0], then the pivots after s0 -- upd()): every store
+    // of the pass has landed and every wave's fixm copies are in
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    constexpr int NK = NB / 16;
+    for (int f = 0; f < nf; ++f) {
+        int meta;
+        asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(meta) : "v"(lds_off(&fmeta[f])) : "memory");
+        meta = __builtin_amdgcn_readfirstlane(meta);
+        const int s0 = meta & 255;
+        double mk[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k) mk[k] = lds_ld64(lds_off(&fixm[f][16 * k + (lane & 15)]));
+        double y = pick_p<0, NB, NB>(p, s0);
+        fix_chain_dpp<NB>(y, mk, p, s0);
+        if (cok) Tout[(r0 + (meta >> 8)) * ld + col] = y;
+    }
+    if (ovf) fix_rows<NB>(P, M, Tout, ld, col, cok, p, mysr, r0, r1, 0, 0, ovf);
 #endif
 #ifdef SWEEP_PROBE_NO_TAIL
     if (nd > 0) return;                          // timing probe only: results NOT kept

@@ -9,7 +9,7 @@ wl=$1; n=$2; shift 2
 for i in $(seq 1 "$n"); do
   for setting in "$@"; do
     s=$setting; [ "$s" = "-" ] && s=""
-    env $s timeout -k 10 200 python bench.py --workload "$wl" --no-cfg3 --no-cpu-baseline --steps 40 --warmup 5 > gpurun_out/ab.json 2> gpurun_out/ab.err
+    env $s timeout -k 10 200 python bench.py --workload "$wl" --no-cfg3 --no-cpu-baseline --steps 64 --warmup 5 --profile-every 1 > gpurun_out/ab.json 2> gpurun_out/ab.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "$wl [$setting] rc=$rc" | tee -a gpurun_out/ab.txt; tail -3 gpurun_out/ab.err; exit $rc; fi
     python -c "

@@ -101,3 +101,38 @@ def test_cpu_baseline_mid_run_sample():
     assert r["kind"] == "port" and r["cores"] == 1 and r["value"] > 0
     assert "seconds_per_pivot_at_1" in r and "seconds_per_pivot_at_4" in r
     assert r["seconds_per_pivot"] == r["seconds_per_pivot_at_4"]
+
+
+class _FakeEngine:
+    """records put_rows / run calls (bench's device warm-up and upload)"""
+
+    def __init__(self, pivots_left=10 ** 9):
+        self.puts, self.runs, self.left = [], [], pivots_left
+
+    def put_rows(self, row0, rows):
+        self.puts.append((row0, rows.shape[0], float(rows[0, 0])))
+
+    def run(self, rule, k):
+        done = min(k, self.left)
+        self.left -= done
+        self.runs.append(k)
+        return 0, done
+
+
+def test_device_warmup_runs_whole_groups_and_stops_when_the_lp_ends():
+    assert bench.device_warmup(None, 64, 150.0) == {"ms": 0.0, "groups": 0}
+    h = _FakeEngine(pivots_left=64 * 20)
+    r = bench.device_warmup(h, 64, 1e6)
+    assert r["groups"] == 20 and h.runs == [512, 512, 512]
+    h = _FakeEngine()
+    r = bench.device_warmup(h, 64, 0.0)
+    assert r["groups"] == 0 and h.runs == []
+
+
+def test_upload_feeds_the_heater_the_same_rows_locally_numbered():
+    kind, m, ns, n, a0, a1 = bench.workload("cfg3", 2, 1)
+    e, h = _FakeEngine(), _FakeEngine()
+    bench.upload([e], kind, m, ns, [(a0, a1)], blk=1024, heaters=[h])
+    assert [p[0] for p in e.puts] == [0] + [1 + a for a in range(a0, a1, 1024)]
+    assert [p[0] for p in h.puts] == [0] + [1 + a - a0 for a in range(a0, a1, 1024)]
+    assert [p[1:] for p in e.puts] == [p[1:] for p in h.puts]
