@@ -2130,6 +2130,14 @@ __device__ __forceinline__ int next_pivot_row(u64 &h, long long mysr, int &row)
     h &= ~same;
     return 63 - __builtin_clzll(same);
 }
+// lane l's double, wave-uniform
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 // p[s0] for a wave-uniform s0: a tree of uniform branches (no per-element
 // selects)
 template <int L, int N, int NB>
@@ -2198,14 +2206,14 @@ template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-           int nstrips, long long run, long long tail, long long tcol, int nexp)
+           int nstrips, long long run, long long tail, long long tcol, long long tend, int nexp)
 {
     // tail > 0: the grid covers strips [0, nstrips) of the columns and the 64
     // columns from tcol (the tableau's last columns: n + 1 is rarely a
     // multiple of 64 W; the pitch's padding columns are 0 and stay 0, never
-    // swept) are dealt out `tail` rows to every block, one 8-row batch per
-    // wave -- a strip of its own would give those few columns a whole block
-    // per row run (cfg4: 30 of 510 resident slots)
+    // swept; tend: one past the last column) are dealt out `tail` rows to
+    // every block -- a strip of its own would give those few columns a whole
+    // block per row run (cfg4: 30 of 510 resident slots)
     constexpr int RW = 8;                        // rows per batch
     constexpr int NC = NB / 2;                   // multiplier registers (2 pivots x 8 rows each)
     constexpr int XS = W * RW * 64;              // doubles of a slot's rows (W waves x 8 rows x 64 columns)
@@ -2451,6 +2459,36 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     if (nd > 0) return;                          // timing probe only: results NOT kept
 #endif
     if (t0 >= t1) return;                        // block-uniform: no tail piece
+    if (tend - tcol <= 4) {
+        // ---- the tail piece of a few columns [tcol, tend) (cfg3, cfg4: one),
+        //      rows across lanes: lane l of wave w takes row t0 + 64 w + l,
+        //      its 64 multipliers and P[s] at the column (a per-pivot scalar,
+        //      broadcast by readlane) -- one memory round trip, then upd()'s
+        //      chain in pivot order with the pivot rows' P[s] taken in it
+        //      (the chain of one(); no fix-up after).  (Columns across lanes,
+        //      below: 1 useful lane in 64 and a round trip per 8 rows, plus
+        //      the pivot rows' -- 10 us of the cfg4 launch)
+        if (64 * wave < t1 - t0) {               // wave-uniform
+            const long long rw = t0 + 64 * wave + lane;
+            const bool rok = rw < t1;
+            const long long rr = rok ? rw : t1 - 1;
+            const int rri = (int)rr;
+            double m[NB];
+#pragma unroll
+            for (int s = 0; s < NB; ++s) m[s] = M[mq(rr, s)];
+            for (long long c = tcol; c < tend; ++c) {
+                double x = T[rr * ld + c];
+                const double pv = lane < NB ? P[(long long)lane * ld + c] : 0.0;
+#pragma unroll
+                for (int s = 0; s < NB; ++s) {
+                    const double ps = readlane_f64(pv, s);
+                    x = rri == __builtin_amdgcn_readlane((int)(unsigned)mysr, s) ? ps : fma(-m[s], ps, x);
+                }
+                if (rok) Tout[rr * ld + c] = x;
+            }
+        }
+        return;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ---- the tail piece: the 64 columns from tcol (one per lane) of rows
     //      [t0, t1), wave w on batches t0 + 8 w, t0 + 8 (w + W), ...: the same
@@ -2852,7 +2890,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
         int grpv = grp, nsv = (int)nsg;
-        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &nexp};
+        long long tend = ncol;
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &tend, &nexp};
         const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
         return err != hipSuccess ? err : hipGetLastError();
     }

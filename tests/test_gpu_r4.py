@@ -182,3 +182,33 @@ def test_cfg3_reference_prefix_full_group():
     o.run(0, fx["k"])
     assert _bits_equal(e.download(), o.T)
     e.close()
+
+
+# (kind, m, ns): the k_sweep_rl tail -- the last n + 1 - 64 W floor((n + 1) /
+# 64 W) columns dealt out to every workgroup -- at 1, 2, 4 columns (rows
+# across lanes, one chain per row with the pivot rows' P[s] taken in it) and
+# 5, 33, 64 (columns across lanes); 4-wave (mixed, 1000 rows: 256-column
+# strips) and 8-wave workgroups (tall, 16500 rows: 512-column strips)
+TAILS = [("mixed", 1000, 24), ("mixed", 1000, 25), ("mixed", 1000, 27), ("mixed", 1000, 28),
+         ("mixed", 1000, 56), ("mixed", 1000, 87), ("tall", 16500, 512), ("tall", 16500, 514),
+         ("tall", 16500, 551)]
+
+
+@pytest.mark.parametrize("kind,m,ns", TAILS)
+def test_sweep_tail_columns(kind, m, ns):
+    """the sweep's tail piece, rows across lanes (<= 4 columns) and columns
+    across lanes (more): 2 full groups and a padded one at depth 64, every
+    bit (signed zeros included) as oracle/lp_f64.c's, no fallback"""
+    T = gen.tableau(kind, m, ns, 31)
+    W = 8 if m >= 16384 else 4
+    rest = T.shape[1] % (64 * W)
+    assert T.shape[1] >= 64 * W and rest == {24: 1, 25: 2, 27: 4, 28: 5, 56: 33, 87: 64, 512: 1, 514: 3,
+                                             551: 40}[ns]
+    e = _engine(T, 64)
+    o = F64Tableau(T)
+    st, done = e.run(_lib.RULE_STANDARD, 150)
+    ost, olog = o.run(0, 150)
+    assert done == len(olog) and e.log().tolist() == olog.tolist()
+    assert _bits_equal(e.download(), o.T)
+    assert e.exchange_path()[1] == 0
+    e.close()
