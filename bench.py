@@ -517,7 +517,9 @@ def main():
         gpus = [None] * world
         dist.all_gather_object(gpus, (os.uname().nodename, device))
         heater = None
-        if args.device_warmup_ms > 0 and len(set(gpus)) == world:
+        # (LPGPU_BENCH_FORCE_HEAT=1: warm up anyway -- rehearses this path with
+        # co-located ranks on a workload whose selections fit one XCD together)
+        if args.device_warmup_ms > 0 and (len(set(gpus)) == world or os.environ.get("LPGPU_BENCH_FORCE_HEAT") == "1"):
             heater = _lib.Engine(re_ - rb, n, device=device)
             heater.set_block(B)
         upload([eng], kind, m, ns, [(rb, re_)], heaters=[heater])
