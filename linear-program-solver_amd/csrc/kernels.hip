@@ -1994,9 +1994,9 @@ __device__ __forceinline__ void rg_pair(double (&x)[8], double m, double pa, dou
 //   (exact no-ops); shorter ones take k_sweep_dp2 at their own depth
 //   (launch_sweep).  Every element gets exactly
 //   upd()'s float64 operations in pivot order: bit-identical to
-//   oracle/lp_f64.c.  cfg4 (W = 8, D = 4, 254 VGPRs, one workgroup per CU):
-//   884 us per 64-pivot launch = 0.61 of the HBM spec; cfg3 (W = 4, D = 2):
-//   139 us = 0.49 (profiles/r03/kernel_stats_r03_final.csv).
+//   oracle/lp_f64.c.  cfg4 (W = 8, D = 4, 243 VGPRs, one workgroup per CU):
+//   847 us per 64-pivot launch = 0.64 of the HBM spec; cfg3 (W = 4, D = 2):
+//   109 us = 0.62 (profiles/r04/kernel_stats_r04b_final.csv).
 // ---------------------------------------------------------------------------
 // LDS byte offset of a __shared__ location (for LDS accesses written in asm)
 __device__ __forceinline__ unsigned lds_off(const double *p)

@@ -219,8 +219,8 @@ for step in "$@"; do
             # (FETCH_SIZE and WRITE_SIZE do not fit one pass), one workload a run
             export TMPDIR=/tmp
             for W in ${PMC_WORKLOADS:-cfg4 cfg3}; do
-                run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
-                run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline
+                run pmc_fetch_$W 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline --device-warmup-ms 0
+                run pmc_write_$W 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$W" -o run -- python3 "$PWD/bench.py" --workload $W --no-cfg3 --steps 8 --warmup 2 --no-cpu-baseline --device-warmup-ms 0
                 PB=64   # the engine's auto pivots per sweep (cfg4 and, since round 3, cfg3)
                 run pmc_json_$W 120 python scripts/hbm_traffic.py "$OUT/pmc_fetch_$W" "$OUT/pmc_write_$W" "$OUT/hbm_traffic.json" --block $PB --kernel k_sweep_rl --workload $W
             done ;;
