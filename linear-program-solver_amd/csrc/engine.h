@@ -173,6 +173,14 @@ struct Args {
     // rank's (peer[rank] == xbuf), written by the peers over xGMI
     unsigned long long *xbuf;
     unsigned long long *const *peer;
+    // out-of-place sweep (k_sweep_rl, LPGPU_SWEEP_OOP): the pass reads T and
+    // writes Tout (the handle's other tableau buffer; Tout == T: in place), and
+    // block 0 of a sweep that ran stores flipseq into *dflips -- the host's
+    // record of which buffer holds the tableau after a batch (a sweep skipped
+    // because the solve ended or a group timed out leaves the previous one)
+    double *Tout;
+    unsigned *dflips;
+    unsigned flipseq;
 };
 
 // exchange buffer layout (granules of 8 bytes), see kernels.hip (XR)
@@ -202,13 +210,14 @@ hipError_t launch_ratio(hipStream_t s, const Args &A, int t, int grp, int mode, 
 hipError_t launch_pick(hipStream_t s, const Args &A, int t, int mode);
 hipError_t launch_gather(hipStream_t s, const Args &A, int t);
 hipError_t launch_prow(hipStream_t s, const Args &A, int t, int grp, int rsrc, int peek);
-// T <- T with the group's pivots, in place; nd_max >= ndef: the handle's
+// T <- T with the group's pivots (k_sweep_rl with A.Tout != A.T: into Tout,
+// *flipped = true; every other sweep in place); nd_max >= ndef: the handle's
 // pivots per sweep; cnt (> 0): the most pivots this group can hold, when the
 // host knows it (a call's last group, an explicit pivot) -- a shallower
 // kernel then, or the padded k_sweep_rl (e0, e1: events recorded at the
 // kernel's start and end, for lp_profile)
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int cnt = -1, hipEvent_t e0 = nullptr,
-                        hipEvent_t e1 = nullptr);
+                        hipEvent_t e1 = nullptr, bool *flipped = nullptr);
 
 constexpr int GROUP_MAXBLOCKS = 256;
 constexpr int GRAN_REGIONS = 4;       // regions of Args::gran (see there)

@@ -1994,9 +1994,10 @@ __device__ __forceinline__ void rg_pair(double (&x)[8], double m, double pa, dou
 //   (exact no-ops); shorter ones take k_sweep_dp2 at their own depth
 //   (launch_sweep).  Every element gets exactly
 //   upd()'s float64 operations in pivot order: bit-identical to
-//   oracle/lp_f64.c.  cfg4 (W = 8, D = 4, 243 VGPRs, one workgroup per CU):
-//   847 us per 64-pivot launch = 0.64 of the HBM spec; cfg3 (W = 4, D = 2):
-//   109 us = 0.62 (profiles/r04/kernel_stats_r04b_final.csv).
+//   oracle/lp_f64.c.  cfg4 (W = 8, D = 4, 243 VGPRs, one workgroup per CU,
+//   out of place: T -> the handle's other buffer, lpgpu.cpp): ~812 us per
+//   64-pivot launch = 0.66 of the HBM spec (in place 842 us); cfg3 (W = 4,
+//   D = 2, in place): 109 us = 0.62 (profiles/r04/README.md).
 // ---------------------------------------------------------------------------
 // LDS byte offset of a __shared__ location (for LDS accesses written in asm)
 __device__ __forceinline__ unsigned lds_off(const double *p)
@@ -2206,7 +2207,8 @@ template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-           int nstrips, long long run, long long tail, long long tcol, long long tend, int nexp)
+           int nstrips, long long run, long long tail, long long tcol, long long tend, int nexp,
+           unsigned *dflips, unsigned flipseq)
 {
     // tail > 0: the grid covers strips [0, nstrips) of the columns and the 64
     // columns from tcol (the tableau's last columns: n + 1 is rarely a
@@ -2244,6 +2246,9 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     if (nd == 0 || ctl->bar_timeout) return;     // nothing deferred / group redone by the host
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // out of place (Tout != T): this sweep ran -- the host's record of which
+    // buffer holds the tableau (every block takes the same branch above)
+    if (dflips && blockIdx.x == 0 && threadIdx.x == 0) *dflips = flipseq;
     if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
     auto srow = [&](int s) -> long long { return sr[s]; };
     const int strip = (int)(blockIdx.x % (unsigned)nstrips);
@@ -2789,8 +2794,10 @@ static int sweep_blocks_per_cu(const void *fn, int threads)
 // path's 32); k_sweep_dp / k_sweep_st stay as A/B variants.  All stores are
 // write-through (sc1): the tableau lines leave the L2 as they are written
 // instead of in the writeback at the kernel's end (profiles/r01/README.md).
-hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int cnt, hipEvent_t e0, hipEvent_t e1)
+hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int cnt, hipEvent_t e0, hipEvent_t e1,
+                        bool *flipped)
 {
+    if (flipped) *flipped = false;
     // the kernel's depth: the group's known pivot count when the host knows it
     // (a call's last group, explicit pivots), else the handle's depth
     if (cnt > 0 && cnt < nd_max) nd_max = cnt;
@@ -2878,21 +2885,20 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         long long tail = spread ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + 7) / 8 * 8 : 0;
         long long tcol = nfull * 64 * WL;
         const double *T = A.T, *Pp = A.P, *Mp = A.MQ;
-        double *To = A.T;
-#ifdef SWEEP_OOP_PROBE
-        // timing probe only (results are NOT kept): the sweep writes a scratch
-        // copy instead of the tableau, to time an out-of-place pass
-        static double *scratch = nullptr;
-        if (!scratch && hipMalloc(&scratch, (size_t)A.rows * A.ld * sizeof(double)) != hipSuccess) scratch = nullptr;
-        if (scratch) To = scratch;
-#endif
+        // out of place into the handle's other buffer when it has one (the
+        // host then takes Tout as the tableau; see Args::dflips)
+        double *To = (A.Tout && A.Tout != A.T) ? A.Tout : A.T;
+        unsigned *dfl = To != A.T ? A.dflips : nullptr;
+        unsigned fseq = A.flipseq;
         const long long *dRp = A.dR;
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
         int grpv = grp, nsv = (int)nsg;
         long long tend = ncol;
-        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &tend, &nexp};
+        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &tend, &nexp,
+                        &dfl, &fseq};
         const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
+        if (err == hipSuccess && flipped) *flipped = To != A.T;
         return err != hipSuccess ? err : hipGetLastError();
     }
     const long long ns = (A.ld + 127) / 128;

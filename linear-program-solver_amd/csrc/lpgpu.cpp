@@ -40,6 +40,13 @@ struct lp_handle {
     int64_t rb = 0, rc = 0;         // local constraint block [rb, rb+rc)
     int64_t rows = 0;               // local rows = rc + 1
     double *T = nullptr, *P = nullptr, *M = nullptr, *MQ = nullptr, *row0 = nullptr, *col0 = nullptr;
+    // out-of-place sweeps (LPGPU_SWEEP_OOP): two tableau buffers, T is the
+    // current one -- Tb[flips & 1] after `flips` sweeps that wrote the other
+    // (dflips: the device's record of the last one that ran, read at each sync)
+    double *Tb[2] = {nullptr, nullptr};
+    unsigned *dflips = nullptr;
+    unsigned flips = 0, hflips = 0;
+    bool oop = false;
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
     int block = 0;                  // pivots deferred into one sweep (1..BMAX; 0 = auto)
@@ -274,6 +281,9 @@ static Args args_of(const lp_handle *h)
 {
     Args A;
     A.T = h->T;
+    A.Tout = h->oop ? h->Tb[(h->flips + 1) & 1] : h->T;
+    A.dflips = h->dflips;
+    A.flipseq = h->flips + 1;
     A.row0 = h->row0;
     A.col0 = h->col0;
     A.M = h->M;
@@ -410,6 +420,28 @@ static int alloc_handle(lp_handle *h)
     const size_t tbytes = (size_t)h->rows * (size_t)h->ld * sizeof(double);
     HCHK(h, hipMalloc(&h->T, tbytes));
     HCHK(h, hipMemsetAsync(h->T, 0, tbytes, h->s));
+    h->Tb[0] = h->T;
+    {
+        // out-of-place sweeps where the tableau is far beyond the 256 MB
+        // Infinity Cache: cfg4 (2.2 GB) 842 -> 812 us per sweep (0.64 -> 0.66
+        // of the HBM spec, same box); at cfg3's 273 MB the in-place pass keeps
+        // the tableau in the cache for the selection's column reads (OOP:
+        // selection 4.47 -> 4.67 us per pivot, 157k -> 152k pivots/s).
+        // LPGPU_SWEEP_OOP: 1 always, 0 never, unset: by size (> 512 MiB)
+        static const int oop_env = [] {
+            const char *v = std::getenv("LPGPU_SWEEP_OOP");
+            return v ? std::atoi(v) : 2;
+        }();
+        h->oop = oop_env == 1 || (oop_env == 2 && tbytes > ((size_t)512 << 20));
+    }
+    if (h->oop) {
+        // the second buffer: its padding columns stay 0 like T's (no sweep
+        // writes past column n)
+        HCHK(h, hipMalloc(&h->Tb[1], tbytes));
+        HCHK(h, hipMemsetAsync(h->Tb[1], 0, tbytes, h->s));
+        HCHK(h, hipMalloc(&h->dflips, sizeof(unsigned)));
+        HCHK(h, hipMemsetAsync(h->dflips, 0, sizeof(unsigned), h->s));
+    }
     // two sets of group data (P, M, dR, dC) by group parity
     HCHK(h, hipMalloc(&h->P, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double)));
     HCHK(h, hipMemsetAsync(h->P, 0, 2 * (size_t)lpk::BMAX * h->ld * sizeof(double), h->s));
@@ -736,7 +768,9 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->dpeer) (void)hipFree(h->dpeer);
     if (h->xbuf) (void)hipFree(h->xbuf);
     if (h->sx) (void)hipStreamDestroy(h->sx);
-    if (h->T) (void)hipFree(h->T);
+    if (h->Tb[0]) (void)hipFree(h->Tb[0]);
+    if (h->Tb[1]) (void)hipFree(h->Tb[1]);
+    if (h->dflips) (void)hipFree(h->dflips);
     if (h->P) (void)hipFree(h->P);
     if (h->M) (void)hipFree(h->M);
     if (h->MQ) (void)hipFree(h->MQ);
@@ -898,11 +932,11 @@ static int prof_slot(lp_handle *h, hipEvent_t *e0, hipEvent_t *e1, int kind)
 
 // cnt: the most pivots the group can hold (the kernel's depth when below the
 // handle's: a call's last group, an explicit pivot)
-static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, int cnt)
+static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, int cnt, bool *flipped)
 {
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 0));
-    HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), cnt, e0, e1));
+    HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), cnt, e0, e1, flipped));
     return LP_PIVOTED;
 }
 
@@ -1028,8 +1062,16 @@ static int sync_ctl(const Members &M)
     for (lp_handle *h : M) {
         HCHK(h, hipSetDevice(h->dev));
         HCHK(h, hipMemcpyAsync(h->hctl, h->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, h->s));
+        if (h->oop) HCHK(h, hipMemcpyAsync(&h->hflips, h->dflips, sizeof(unsigned), hipMemcpyDeviceToHost, h->s));
     }
     for (lp_handle *h : M) HCHK(h, hipStreamSynchronize(h->s));
+    // out-of-place sweeps: the buffer the last sweep that RAN wrote (sweeps
+    // after a stop or a timed-out group return at once and leave it)
+    for (lp_handle *h : M)
+        if (h->oop && h->hflips != h->flips) {
+            h->flips = h->hflips;
+            h->T = h->Tb[h->flips & 1];
+        }
     return LP_PIVOTED;
 }
 
@@ -1087,9 +1129,20 @@ static int enqueue_select(const Members &M, const std::vector<Args> &A, int t, i
     return LP_PIVOTED;
 }
 
-static int enqueue_sweep(const Members &M, const std::vector<Args> &A, int grp, int cnt)
+// (out of place: a sweep that wrote the other buffer makes it the tableau of
+// every later launch -- the handle's T and the members' Args)
+static int enqueue_sweep(const Members &M, std::vector<Args> &A, int grp, int cnt)
 {
-    for (size_t k = 0; k < M.size(); ++k) CALL(launch_sweep_timed(M[k], A[k], grp, cnt));
+    for (size_t k = 0; k < M.size(); ++k) {
+        lp_handle *h = M[k];
+        bool flipped = false;
+        CALL(launch_sweep_timed(h, A[k], grp, cnt, &flipped));
+        if (flipped) {
+            h->flips += 1;
+            h->T = h->Tb[h->flips & 1];
+            A[k] = args_of(h);
+        }
+    }
     return LP_PIVOTED;
 }
 
@@ -1269,6 +1322,7 @@ static int pivot_loop(lp_handle *h, int mode, int rule, int64_t cap, int64_t lim
             }
         }
         CALL(sync_ctl(M));
+        A = args_all(M);                     // (out of place: the buffer the last sweep that ran wrote)
         bool timed_out = false;
         for (lp_handle *x : M) timed_out = timed_out || x->hctl->bar_timeout != 0;
         if (geo.g > 0 && xr) CALL(agree_on_timeout(h, timed_out));
@@ -1330,7 +1384,7 @@ extern "C" int lp_find_pivot(lp_handle *h, int rule, int do_pivot, int64_t *r, i
     if (rule != LP_RULE_STANDARD && rule != LP_RULE_MIN_INDEX)
         return fail(h, LP_BAD_ARG, "unknown rule");
     const Members M = members_of(h);
-    const std::vector<Args> A = args_all(M);
+    std::vector<Args> A = args_all(M);
     CALL(begin_call(M, A, lpk::MODE_RUN, rule, 0, -1, -1, -1));
     for (size_t k = 0; k < M.size(); ++k) HCHK(M[k], lpk::launch_enter(M[k]->s, A[k]));
     CALL(enqueue_select(M, A, 0, 0, 0, 0, do_pivot == 0));
@@ -1348,7 +1402,7 @@ static int explicit_pivot(lp_handle *h, int64_t r, int64_t c, bool checked)
     if (r < 0 || r >= h->m || c < 0 || c >= h->n)
         return fail(h, LP_BAD_ARG, "pivot index out of range");
     const Members M = members_of(h);
-    const std::vector<Args> A = args_all(M);
+    std::vector<Args> A = args_all(M);
     CALL(begin_call(M, A, lpk::MODE_RUN, LP_RULE_STANDARD, 0, -1, r, c));
     CALL(enqueue_select(M, A, 0, 0, checked ? 1 : 2, 0, false));
     CALL(enqueue_sweep(M, A, 0, 1));

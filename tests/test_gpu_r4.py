@@ -212,3 +212,18 @@ def test_sweep_tail_columns(kind, m, ns):
     assert _bits_equal(e.download(), o.T)
     assert e.exchange_path()[1] == 0
     e.close()
+
+
+def test_out_of_place_sweep_worker():
+    """LPGPU_SWEEP_OOP=1 (k_sweep_rl reads one tableau buffer and writes the
+    other, the host follows the buffer the last sweep that ran wrote): runs,
+    explicit pivots between runs, re-uploads, solves that end inside a batch,
+    a timed-out group redone on the per-pivot kernels -- bit for bit as
+    oracle/lp_f64.c (one child process: the switch is read once per process)"""
+    import os
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(__file__), "_oop_worker.py")
+    env = dict(os.environ, LPGPU_SWEEP_OOP="1")
+    run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=280)
+    assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
