@@ -100,9 +100,31 @@ def timeout_recovery():
     e.close()
 
 
+def shard_group():
+    """in-process row shards (one k_group launch for all members): each
+    member's sweep flips its own buffers"""
+    T = gen.tableau("tall", 3000, 300, 19)
+    o = F64Tableau(T)
+    _, olog = o.run(0, 150)
+    grp = _lib.create_group(T.shape[0] - 1, T.shape[1] - 1, 2)
+    for g in grp:
+        g.upload(T)
+        g.set_block(64)
+    st, done = grp[0].run(_lib.RULE_STANDARD, 150)
+    ok = done == len(olog) and grp[0].log().tolist() == olog.tolist()
+    ok = ok and bits(grp[0].rows(0, 1), o.T[:1])
+    for g in grp:
+        b, c = g.row_begin, g.row_count
+        ok = ok and bits(g.rows(1 + b, c), o.T[1 + b:1 + b + c])
+    check("2 in-process shards", ok)
+    for g in reversed(grp):
+        g.close()
+
+
 if __name__ == "__main__":
     assert os.environ.get("LPGPU_SWEEP_OOP") == "1"
     runs()
     solves()
     timeout_recovery()
+    shard_group()
     print("ALL OK")
