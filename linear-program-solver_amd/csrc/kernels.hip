@@ -2203,6 +2203,9 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
     }
 }
 
+#ifndef SWEEP_LA
+#define SWEEP_LA 0
+#endif
 template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
@@ -2302,14 +2305,14 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             const long long cc = min(colw + 2 * (lane & 31), ld - 2);
             __builtin_amdgcn_global_load_lds(T + row * ld + cc,
                                              (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
-                                             16, 0, 0);
+                                             16, 0, SWEEP_LA);
         }
         // (W >= 4: quads 0, 1 x halves 0, 1 by waves 0..3; more waves re-copy)
         const int w4 = wave & 3;
         const long long qd = min((rb >> 2) + (w4 >> 1), nquad - 1);
         __builtin_amdgcn_global_load_lds(M + qd * (4 * BMAX) + (w4 & 1) * 128 + 2 * lane,
                                          (__attribute__((address_space(3))) void *)&ms[slot][(w4 >> 1) * (4 * BMAX + QP) + (w4 & 1) * 128],
-                                         16, 0, 0);
+                                         16, 0, SWEEP_LA);
     };
     // vector-memory instructions a wave issues per batch after the copies of
     // batch i: the copies of the next batches (5 each) and the stores (8 each)
@@ -2801,7 +2804,10 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
     // the kernel's depth: the group's known pivot count when the host knows it
     // (a call's last group, explicit pivots), else the handle's depth
     if (cnt > 0 && cnt < nd_max) nd_max = cnt;
-    constexpr int W = 8, RW = 4, SA = 16;
+#ifndef SWEEP_SA
+#define SWEEP_SA 16
+#endif
+    constexpr int W = 8, RW = 4, SA = SWEEP_SA;
     // LPGPU_SWEEP_DP (A/B): 1 (default) k_sweep_dp2 up to 48 pivots per sweep and
     // k_sweep_rl at 64 (round 3: cfg4 906-931 against 978-980 us per launch,
     // cfg3 at 64 140 against 149 us; at 48 equal, at 32 96 against 93), 2
@@ -2890,6 +2896,15 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         double *To = (A.Tout && A.Tout != A.T) ? A.Tout : A.T;
         unsigned *dfl = To != A.T ? A.dflips : nullptr;
         unsigned fseq = A.flipseq;
+        // out of place (a tableau far beyond the Infinity Cache): the stores
+        // also non-temporal (SA | 2), so the pass does not evict what the
+        // selection keeps there -- cfg4 sweep 787-806 -> 775-781 us, selection
+        // 7.12-7.15 -> 6.84-6.93 us per pivot (same box); at cfg3 (in place)
+        // they cost the selection its cached tableau (4.50 -> 4.65 us)
+        if (To != A.T) {
+            if (fn == (const void *)&k_sweep_rl<8, 64, 4, SA>) fn = (const void *)&k_sweep_rl<8, 64, 4, SA | 2>;
+            else if (fn == (const void *)&k_sweep_rl<4, 64, DL, SA>) fn = (const void *)&k_sweep_rl<4, 64, DL, SA | 2>;
+        }
         const long long *dRp = A.dR;
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
