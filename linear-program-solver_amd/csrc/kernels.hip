@@ -1995,9 +1995,10 @@ __device__ __forceinline__ void rg_pair(double (&x)[8], double m, double pa, dou
 //   (launch_sweep).  Every element gets exactly
 //   upd()'s float64 operations in pivot order: bit-identical to
 //   oracle/lp_f64.c.  cfg4 (W = 8, D = 4, 243 VGPRs, one workgroup per CU,
-//   out of place: T -> the handle's other buffer, lpgpu.cpp): ~812 us per
-//   64-pivot launch = 0.66 of the HBM spec (in place 842 us); cfg3 (W = 4,
-//   D = 2, in place): 109 us = 0.62 (profiles/r04/README.md).
+//   out of place: T -> the handle's other buffer, lpgpu.cpp, non-temporal
+//   stores): ~775 us per 64-pivot launch = 0.70 of the HBM spec (in place
+//   842 us); cfg3 (W = 4, D = 2, in place): 109 us = 0.62
+//   (profiles/r04/README.md).
 // ---------------------------------------------------------------------------
 // LDS byte offset of a __shared__ location (for LDS accesses written in asm)
 __device__ __forceinline__ unsigned lds_off(const double *p)
