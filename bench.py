@@ -27,7 +27,7 @@ workload's groups on a SCRATCH copy of the tableau: after the idle gap of the
 upload the MI355X runs the sweep 10-15 % slower for ~30 launches whatever the
 data (scripts/ramp_probe2.py); the benchmarked engine still starts its warmup
 steps from the initial tableau.  Every 8th sweep and selection launch (every
-one below 64 steps) inside the timed region records a pair of HIP events at the
+4th below 64 steps) inside the timed region records a pair of HIP events at the
 kernel's start and end (hipExtLaunchKernelGGL on the engine's stream); the
 roofline's achieved bandwidth is the sweep's algorithmic bytes over that
 kernel time.
@@ -442,7 +442,7 @@ def main():
                     help="1-GPU diagnostic: the workload as S in-process row shards on one GPU")
     ap.add_argument("--profile-every", type=int, default=0,
                     help="time every k-th launch of each kernel with HIP events (1 = all; default: "
-                         "every launch for runs under 64 steps, else every 8th)")
+                         "every 4th for runs under 64 steps, else every 8th)")
     ap.add_argument("--device-warmup-ms", type=float, default=150.0,
                     help="before the W warmup steps, keep the GPU busy this long with the same "
                          "workload on a scratch copy of the tableau (0: off; see device_warmup)")
@@ -451,8 +451,10 @@ def main():
                          "exact-Fraction CPU path, one JSON line each")
     args = ap.parse_args()
     if args.profile_every <= 0:
-        # a short run (the driver's 20 steps) would time only a few launches
-        args.profile_every = 1 if args.steps < 64 else 8
+        # a short run (the driver's 20 steps) would time only 2-3 launches at
+        # every 8th; every launch costs cfg3 ~2 % of its wall-clock rate
+        # (events around each 0.4 ms group: 156.3k against 159.4k pivots/s)
+        args.profile_every = 4 if args.steps < 64 else 8
     if args.configs:
         config_table()
         return
