@@ -303,6 +303,44 @@ __device__ __forceinline__ double dppd(double v)
 // wave minimum (all 64 lanes active), wave-uniform: two quad permutes and two
 // row rotates reduce each row of 16, two row broadcasts fold the rows into
 // lane 63 (the other lanes end with partial or undefined values)
+#ifndef SEL_WMIN_U32
+#define SEL_WMIN_U32 0
+#endif
+#if SEL_WMIN_U32
+// the same minimum over 32-bit order keys (a double's bits with the sign
+// folded so that unsigned order is numeric order): the high words first, then
+// the low words of the lanes that hold the high minimum; each step is ONE
+// v_min_u32 with its DPP operand (the f64 form needs two 32-bit DPP moves and
+// a v_min_f64 per step).  -0.0 orders below +0.0 here; every use of the
+// result only compares it, where the two are equal.
+__device__ __forceinline__ unsigned wumin63(unsigned x)
+{
+    asm("s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        "s_nop 1\n"
+        : "+v"(x));
+    return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ double wmin(double v)
+{
+    const unsigned hi = hi32(v), lo = lo32(v), sg = (unsigned)((int)hi >> 31);
+    const unsigned hk = hi ^ (sg | 0x80000000u);
+    const unsigned hm = wumin63(hk);
+    const unsigned lm = wumin63(hk == hm ? lo ^ sg : 0xffffffffu);
+    const unsigned nn = (unsigned)((int)hm >> 31);          // all ones: the minimum is >= +0
+    return mk_d(lm ^ ~nn, hm ^ (nn ? 0x80000000u : 0xffffffffu));
+}
+#else
 __device__ __forceinline__ double wmin(double v)
 {
     v = vmin(v, dppd<0xB1, 0xf>(v));
@@ -313,6 +351,7 @@ __device__ __forceinline__ double wmin(double v)
     v = vmin(v, dppd<0x143, 0xc>(v));
     return rl_d(lo32(v), hi32(v), 63);
 }
+#endif
 // lane l's word of a summary assembled from wave-uniform values: v_writelane
 // per word (a select chain on the lane index compiled to a branch per word)
 template <int L>
@@ -804,18 +843,80 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         }
         SEL_CLK(6);
         SEL_EV(3);
-        const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
-        const double g = wmin(rl);
+        // ---- pivot row on the own columns: prow(Rl, av) = current values of
+        //      local row Rl (stored row, or P[s*] if it was pivot row s* of
+        //      this launch, + the later pivots of the launch) / av.  In two
+        //      halves: prow_issue(Rl) sends the loads, prow_finish(av) runs
+        //      the chain (the plain path issues them as soon as the leaving
+        //      row is known, before the rest of the decision)
         long long R = NONE;                   // this device's leaving row (XR: its candidate)
         double aR = 0.0, bR = 0.0;
+        double pv[IPL];
+        double p0 = 0.0;
+        double px[IPL], pmr[NK];
+        int psst = -1;
+        auto prow_issue = [&](long long Rl) {
+            const u64 rp = __ballot(lane < t && sRv == Rl);
+            psst = rp ? 63 - __builtin_clzll(rp) : -1;             // uniform
+            // every load issued before any select (see the column's)
+            const double *const xr = Tb + Rl * ld;                 // wave-uniform
+            const double *const mrp = Mb + Rl;
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) px[k] = *gp(at(xr, xoff[k]));
+#pragma unroll
+            for (int k = 0; k < NK; ++k) pmr[k] = ld_sc1(at(mrp, mroff[k]));
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto prow_finish = [&](double avv) {
+            const int sst = psst;
+            double x[IPL], mr[NK];
+            // while the row travels: column 0's pivot value (every block),
+            // computed here (the compiler would sink it to its first use, on
+            // the way to the row-0 summary)
+            if constexpr (!XR) {
+                p0 = bR / aR;
+                asm volatile("" : "+v"(p0));
+            }
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) x[k] = sst >= 0 ? lP[kc[k] * CS + sst] : (cok[k] ? px[k] : 0.0);
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int s = 16 * k + (lane & 15);
+                mr[k] = (s < t && s > sst) ? pmr[k] : 0.0;
+            }
+            if (STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: the row has arrived
+            SEL_CLK(8);
+            row_chain<IPL, NB>(x, mr, lP, kc, t);
+            SEL_DONE(x[IPL - 1]);
+            SEL_CLK(9);
+            // every lane divides (the IPL divisions interleave; a branch
+            // around each made them run one after another), then selects
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                double qd = x[k] / avv;
+                asm("" : "+v"(qd));
+                pv[k] = (jk[k] == C) ? 1.0 : qd;
+            }
+            SEL_DONE(pv[IPL - 1]);
+            SEL_CLK(10);
+        };
+        auto prow = [&](long long Rl, double avv) {
+            prow_issue(Rl);
+            prow_finish(avv);
+        };
+        const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
+        const double g = wmin(rl);
         if (g < INFINITY) {
             const double thr = tie_band(g, tol.ratio_tie);
             const int bs = __builtin_ctzll(__ballot((unsigned)lane < G && rl <= thr));
+            // (block bs has a candidate: its minimum is finite)
+            const long long Rc = un_idx(rl32(w[2], bs));
+            if constexpr (!XR && !XS) prow_issue(Rc);
             aR = rl_d(w[3], w[4], bs);
             bR = rl_d(w[5], w[6], bs);
             const double qR = rl_d(w[7], w[8], bs);
             if (qR <= thr) {                  // block bs's candidate lies inside the global band
-                R = un_idx(rl32(w[2], bs));
+                R = Rc;
             } else {
                 // rare: block bs's first row inside the global band is not its
                 // candidate; it answers with that row (one more hand-off)
@@ -838,49 +939,13 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 R = (long long)rl32(y[0], 0);
                 aR = rl_d(y[1], y[2], 0);
                 bR = rl_d(y[3], y[4], 0);
+                if constexpr (!XR && !XS) prow_issue(R);
             }
         } else if (!XR && !XS) {
             status = LP_UNBOUNDED;
             break;
         }
         SEL_CLK(7);
-        // ---- pivot row on the own columns: prow(Rl, av) = current values of
-        //      local row Rl (stored row, or P[s*] if it was pivot row s* of
-        //      this launch, + the later pivots of the launch) / av
-        double pv[IPL];
-        double p0 = 0.0;
-        auto prow = [&](long long Rl, double avv) {
-            const u64 rp = __ballot(lane < t && sRv == Rl);
-            const int sst = rp ? 63 - __builtin_clzll(rp) : -1;   // uniform
-            // every load issued before any select (see the column's)
-            const double *const xr = Tb + Rl * ld;                 // wave-uniform
-            const double *const mrp = Mb + Rl;
-            double x[IPL];
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) x[k] = *gp(at(xr, xoff[k]));
-            double mr[NK];
-#pragma unroll
-            for (int k = 0; k < NK; ++k) mr[k] = ld_sc1(at(mrp, mroff[k]));
-            __builtin_amdgcn_sched_barrier(0);
-            // while the row travels: column 0's pivot value (every block)
-            if constexpr (!XR) p0 = bR / aR;
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) x[k] = sst >= 0 ? lP[kc[k] * CS + sst] : (cok[k] ? x[k] : 0.0);
-#pragma unroll
-            for (int k = 0; k < NK; ++k) {
-                const int s = 16 * k + (lane & 15);
-                mr[k] = (s < t && s > sst) ? mr[k] : 0.0;
-            }
-            if (STAMPS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // diagnostic: the row has arrived
-            SEL_CLK(8);
-            row_chain<IPL, NB>(x, mr, lP, kc, t);
-            SEL_DONE(x[IPL - 1]);
-            SEL_CLK(9);
-#pragma unroll
-            for (int k = 0; k < IPL; ++k) pv[k] = (jk[k] == C) ? 1.0 : x[k] / avv;
-            SEL_DONE(pv[IPL - 1]);
-            SEL_CLK(10);
-        };
         double gR = g;                        // the device's minimum (XS: over its shards)
         double lps = INFINITY;                // XS: lane x < 8 holds shard x's minimum
         bool win = true;                      // this rank holds the leaving row
@@ -1151,7 +1216,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
             p0 = bR / aR;
         } else if constexpr (!XS) {
-            prow(R, aR);
+            prow_finish(aR);                  // (loads issued at the decision)
         }
         // ---- P[t], row 0 and column 0 (every block: p0 = b / a).  P[t] is
         //      read from pivot t + 2 on (drained with pivot t + 1's ratio

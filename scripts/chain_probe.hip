@@ -124,6 +124,56 @@ __global__ void __launch_bounds__(64) probe(double *out, const double *in, unsig
                 a = __builtin_fma(-s, m, a);
             }
         }
+    } else if constexpr (K == 10) {    // dependent v_fmac_f64 with a scalar (SGPR) operand
+        const long long pu = __builtin_amdgcn_readfirstlane((int)__double_as_longlong(p)) |
+                             ((long long)__builtin_amdgcn_readfirstlane((int)(__double_as_longlong(p) >> 32)) << 32);
+        for (int i = 0; i < NREP; ++i) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) asm volatile("v_fmac_f64 %0, %1, %2" : "+v"(a) : "s"(pu), "v"(m));
+        }
+    } else if constexpr (K == 11) {    // dependent v_min_f64 (no DPP)
+        for (int i = 0; i < NREP; ++i) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) asm volatile("v_min_f64 %0, %0, %1" : "+v"(a) : "v"(m));
+        }
+    } else if constexpr (K == 12) {    // v_mov_b32_dpp quad_perm pair + v_min_f64 (one wmin step), x6
+        for (int i = 0; i < NREP; ++i) {
+            asm volatile("s_nop 1\n"
+                         "v_mov_b32_dpp %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+                         "v_mov_b32_dpp %2, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+                         : "+v"(a), "=v"(r) : "v"(m), "v"(p));
+        }
+    } else if constexpr (K == 13) {    // wave minimum: order key, two u32 passes of single v_min_u32_dpp steps
+        for (int i = 0; i < NREP; ++i) {
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(a);
+            const unsigned hi = (unsigned)(bits >> 32), lo = (unsigned)bits;
+            const unsigned sg = (unsigned)((int)hi >> 31);
+            unsigned hk = hi ^ (sg | 0x80000000u), lk = lo ^ sg;
+#define UMIN1(X)                                                                                       \
+    asm("s_nop 1\n"                                                                                   \
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"                  \
+        "s_nop 1\n"                                                                                   \
+        "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"                  \
+        "s_nop 1\n"                                                                                   \
+        "v_min_u32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n"                            \
+        "s_nop 1\n"                                                                                   \
+        "v_min_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n"                            \
+        "s_nop 1\n"                                                                                   \
+        "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"                         \
+        "s_nop 1\n"                                                                                   \
+        "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"                         \
+        "s_nop 1\n"                                                                                   \
+        : "+v"(X))
+            unsigned hr = hk;
+            UMIN1(hr);
+            const unsigned hmin = __builtin_amdgcn_readlane(hr, 63);
+            unsigned lr = hk == hmin ? lk : 0xffffffffu;
+            UMIN1(lr);
+            const unsigned lmin = __builtin_amdgcn_readlane(lr, 63);
+            const unsigned s2 = (hmin >> 31) ? 0x80000000u : 0xffffffffu;
+            const unsigned long long kk = ((unsigned long long)(hmin ^ s2) << 32) | (lmin ^ ((hmin >> 31) ? 0u : 0xffffffffu));
+            a = __longlong_as_double((long long)kk) + (double)(lane & 1);
+        }
     } else if constexpr (K == 9) {     // ballot + ctz + readlane (first lane with a property)
         for (int i = 0; i < NREP; ++i) {
             const unsigned long long bm = __ballot(a < p);
@@ -155,7 +205,8 @@ int main()
     const char *names[] = {"fmac_f64 dep x8",  "fmac_f64_dpp dep x8", "fmac_f64_dpp 2 chains x4",
                            "div_f64 dep x2",    "wave_min f64 (dpp64)", "wave_min 2x u32 key",
                            "store+vmcnt(0)",    "load sc1 dep (L2)",   "readlane bcast+fma x8",
-                           "ballot+ctz+readlane"};
+                           "ballot+ctz+readlane", "fmac_f64 sgpr dep x8", "v_min_f64 dep x8",
+                           "2 dpp movs (issue)", "wave_min u32 dpp-min asm"};
     auto run = [&](auto kern, int k) {
         std::vector<unsigned long long> c(G);
         for (int rep = 0; rep < 3; ++rep) {
@@ -176,5 +227,8 @@ int main()
     run(probe<7>, 7);
     run(probe<8>, 8);
     run(probe<9>, 9);
+    run(probe<10>, 10);
+    run(probe<11>, 11);
+    run(probe<13>, 13);
     return 0;
 }

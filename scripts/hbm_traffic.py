@@ -1,7 +1,7 @@
 """HBM bytes per sweep (k_sweep_dp) launch from two rocprofv3 --pmc passes.
 
 FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950 (TCC slots), so
-scripts/gpu_run.sh runs bench.py twice under rocprofv3, once per counter.
+scripts/gpu.sh (step pmc) runs bench.py twice under rocprofv3, once per counter.
 Both counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
 wide coalesced streaming read, so it is doubled (MI355X_MICROARCH.md §HBM).
 

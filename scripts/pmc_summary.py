@@ -1,5 +1,5 @@
 """Mean PMC counter values per dispatch of the kernels matching a name, from
-rocprofv3 --pmc output directories (scripts/pmc_pass.sh).
+rocprofv3 --pmc output directories (scripts/gpu.sh step pmcx).
 
 usage: python scripts/pmc_summary.py <dir> [<dir> ...] --kernel k_sweep_rl"""
 import argparse

@@ -7,6 +7,7 @@ Run from the repo root (needs /root/reference, read-only):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --extra   # r2.json only
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline 10   # r3.json only
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline-prefix 64   # r4.json, checkpointed
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline-prefix 80 --out r5.json
 
 It imports the reference, drives its own ``Tableau``/``Simplex`` on inputs
 from this repo's generator (``lpsol_amd.generators``) or on hand-built LPs,
@@ -341,7 +342,7 @@ def headline_main(k: int):
         json.dump({"standard_k": [fx]}, f, separators=(",", ":"))
 
 
-def headline_prefix_main(k: int):
+def headline_prefix_main(k: int, out: str = "r4.json"):
     """tests/golden/r4.json: the same reference walk as ``headline_main`` on
     the cfg3 bench tableau, extended towards one full 64-pivot bench group and
     CHECKPOINTED: after every reference pivot the prefix so far (sequence and
@@ -354,7 +355,7 @@ def headline_prefix_main(k: int):
     del rows
     log = []
     s = bare_simplex(t, log)
-    path = os.path.join(OUT, "r4.json")
+    path = os.path.join(OUT, out)
     t0 = time.time()
     end = None
     times = []
@@ -388,9 +389,12 @@ def main():
     ap.add_argument("--headline-prefix", type=int, default=0, metavar="K",
                     help="only tests/golden/r4.json: up to K reference pivots on the cfg3 bench "
                          "tableau, rewritten after every pivot")
+    ap.add_argument("--out", default="r4.json",
+                    help="--headline-prefix: the fixture file under tests/golden/ (r5.json: K = 80, across "
+                         "the first sweep boundary)")
     args = ap.parse_args()
     if args.headline_prefix:
-        headline_prefix_main(args.headline_prefix)
+        headline_prefix_main(args.headline_prefix, args.out)
         return
     if args.extra:
         extra_main()
