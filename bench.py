@@ -351,11 +351,30 @@ def accounting(steps: int, block: int, elapsed: float, sweep_avg_ms: float, sel_
     }
 
 
+def dump_stamps(eng, geo: dict, block: int, rank: int) -> None:
+    """diagnostic builds only (LPGPU_STAMPS=1 with variants/stamps.so): the
+    last selection launch's phase clocks of this rank into
+    $LPGPU_STAMPS_DUMP/stamps_rank<r>.npz (scripts/sel_clocks.py --file)"""
+    d = os.environ.get("LPGPU_STAMPS_DUMP")
+    if not d or os.environ.get("LPGPU_STAMPS") != "1":
+        return
+    import ctypes
+    buf = (ctypes.c_longlong * (256 * 64 * 4))()
+    if eng.lib.lpdiag_bstamps(eng.h, buf) != 0:
+        return
+    os.makedirs(d, exist_ok=True)
+    np.savez(os.path.join(d, f"stamps_rank{rank}.npz"), buf=np.array(buf, dtype=np.int64),
+             blocks=int(geo["blocks"]), block=int(block),
+             geometry=np.array([geo.get(k, 0) for k in ("blocks", "ipl", "xcd_shards")]))
+
+
 def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int, heater=None, heat_ms: float = 0.0):
-    """device warm-up on the heater (untimed, another tableau), warmup groups,
-    then exactly `steps` timed groups bracketed by the barrier + stream sync
+    """device warm-up on the heater (untimed, another tableau; closed right
+    after it), warmup groups, then exactly `steps` timed groups bracketed by the barrier + stream sync
     (lp_run ends with a stream sync)."""
     heat = device_warmup(heater, block, heat_ms)
+    if heater is not None:
+        heater.close()                           # its buffers leave before the timed groups (ADVICE r4)
     barrier()                                    # ranks enter the warmup together (the exchange needs all)
     st, done = eng.run(_lib.RULE_STANDARD, warmup * block)
     if done != warmup * block:
@@ -397,8 +416,6 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
     xw0 = engs[0].xwait()
     elapsed, sw_ms, sel_ms, sw_n, sel_n, heat = timed_run(engs[0], steps, warmup, block, lambda: None, every,
                                                           heater, heat_ms)
-    if heater is not None:
-        heater.close()
     xw1 = engs[0].xwait()
     path, fallbacks = engs[0].exchange_path()
     geo = engs[0].geometry()
@@ -532,9 +549,7 @@ def main():
         xw0 = eng.xwait()
         elapsed, sw_ms, sel_ms, sw_n, sel_n, heat = timed_run(eng, args.steps, args.warmup, B, dist.barrier,
                                                               args.profile_every, heater, args.device_warmup_ms)
-        if heater is not None:
-            heater.close()
-        elif args.device_warmup_ms > 0:
+        if heater is None and args.device_warmup_ms > 0:
             heat["skipped"] = "ranks share a GPU"
         xw1 = eng.xwait()
         # the cross-rank hop per pivot (block 0: its summary sent -> the
@@ -547,6 +562,7 @@ def main():
         # and the selection kernel every rank actually ran (its last launch)
         path, fallbacks = eng.exchange_path()
         geo = eng.geometry()
+        dump_stamps(eng, geo, B, rank)
         kern = geo["kernel"] + (f" as {geo['xcd_shards']} XCD shards" if geo.get("xcd_shards") else
                                 " on one XCD" if geo.get("on_one_xcd") else "")
         ids = [None] * world

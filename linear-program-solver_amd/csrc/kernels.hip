@@ -2468,7 +2468,11 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     if (nd > 0) return;                          // timing probe only: results NOT kept
 #endif
     if (t0 >= t1) return;                        // block-uniform: no tail piece
-    if (tend - tcol <= 4) {
+    // (rows across lanes only where the block's W waves cover its tail in
+    // one pass; a longer tail -- tall tableaux on few blocks -- takes the
+    // columns-across-lanes loop below, ADVICE r4.  A loop here instead cost
+    // the whole kernel scalar registers: cfg3 108 -> 110 us.)
+    if (tend - tcol <= 4 && t1 - t0 <= 64LL * W) {
         // ---- the tail piece of a few columns [tcol, tend) (cfg3, cfg4: one),
         //      rows across lanes: lane l of wave w takes row t0 + 64 w + l,
         //      its 64 multipliers and P[s] at the column (a per-pivot scalar,
@@ -2776,6 +2780,19 @@ static int sweep_cus()
 
 // resident sweep workgroups per CU: the runtime's occupancy answer for the
 // compiled kernel (cached per kernel)
+// the CUs a sweep grid is sized for: all of them (tests: LPGPU_SWEEP_CUS
+// sizes it for fewer -- longer row runs and tail pieces per block than any
+// real device gives at test sizes)
+static int sweep_grid_cus()
+{
+    static int ncu = 0;
+    if (ncu == 0) {
+        ncu = sweep_cus();
+        if (const char *v = std::getenv("LPGPU_SWEEP_CUS"))
+            if (std::atoi(v) > 0) ncu = std::min(ncu, std::atoi(v));
+    }
+    return ncu;
+}
 static int sweep_blocks_per_cu(const void *fn, int threads)
 {
     static std::mutex mu;
@@ -2882,7 +2899,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         const long long ncol = A.n + 1, nfull = ncol / (64 * WL), rest = ncol - nfull * 64 * WL;
         const bool spread = rl_tail != 0 && nfull >= 1 && rest > 0 && rest <= 64;
         const long long nsg = spread ? nfull : (ncol + 64 * WL - 1) / (64 * WL);
-        const long long slots = (long long)sweep_cus() * bpc;
+        const long long slots = (long long)sweep_grid_cus() * bpc;
         long long nrun = slots / nsg;
         if (nrun < 1) nrun = 1;
         long long run = (A.rows + nrun - 1) / nrun;
@@ -2958,7 +2975,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
             const char *v = std::getenv("LPGPU_SWEEP_TAIL");
             tail_env = v ? std::atoi(v) : 1;
         }
-        const long long slots = (long long)sweep_cus() * bpc;
+        const long long slots = (long long)sweep_grid_cus() * bpc;
         const bool tailed = ns >= 2 && (tail_env == 2 || (tail_env == 1 && A.rows * (ns - 1) >= 2048 * slots));
         const long long nsg = tailed ? ns - 1 : ns;   // strips with blocks of their own
         long long nrun = slots / nsg;
@@ -2981,7 +2998,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         return err != hipSuccess ? err : hipGetLastError();
     }
     const int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
-    long long nrun = (long long)sweep_cus() * bpc / ns;
+    long long nrun = (long long)sweep_grid_cus() * bpc / ns;
     if (nrun < 1) nrun = 1;
     long long run = (A.rows + nrun - 1) / nrun;
     run = (run + RW - 1) / RW * RW;

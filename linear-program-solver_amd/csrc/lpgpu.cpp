@@ -226,21 +226,38 @@ struct RcclComm : Comm {
 struct GroupComm : Comm {
     Members all;                   // every shard, rank order
     double **dptrs = nullptr;      // device array of the shards' xg pointers
-    Args *dargs = nullptr;         // device array of the shards' kernel arguments
-    std::vector<Args> hargs;       // pinned-free staging copy (kept alive until the next sync)
+    // the shards' kernel arguments, two slots by group parity (out-of-place
+    // sweeps change them from group to group): a device array each, staged
+    // from pinned host memory, and the event of each slot's last copy -- a
+    // slot is rewritten only after that copy has run
+    Args *dargs = nullptr;
+    Args *hargs = nullptr;
+    hipEvent_t staged[2] = {nullptr, nullptr};
     hipStream_t s = nullptr;       // shared by all shards, released with the last one
     ~GroupComm() override
     {
         if (dptrs) (void)hipFree(dptrs);
         if (dargs) (void)hipFree(dargs);
+        if (hargs) (void)hipHostFree(hargs);
+        for (hipEvent_t e : staged)
+            if (e) (void)hipEventDestroy(e);
         if (s) (void)hipStreamDestroy(s);
     }
-    // the shards' arguments for a one-launch persistent selection
-    int stage_args(lp_handle *h, const std::vector<Args> &A)
+    // the shards' arguments for a one-launch persistent selection of a group
+    // of parity grp; returns the device array through *out
+    int stage_args(lp_handle *h, const std::vector<Args> &A, int grp, Args **out)
     {
-        if (!dargs) HCHK(h, hipMalloc(&dargs, all.size() * sizeof(Args)));
-        hargs = A;
-        HCHK(h, hipMemcpyAsync(dargs, hargs.data(), A.size() * sizeof(Args), hipMemcpyHostToDevice, s));
+        const size_t n = all.size();
+        if (A.size() != n) return fail(h, LP_DEVICE_ERROR, "shard arguments: member count");
+        if (!dargs) HCHK(h, hipMalloc(&dargs, 2 * n * sizeof(Args)));
+        if (!hargs) HCHK(h, hipHostMalloc(&hargs, 2 * n * sizeof(Args), hipHostMallocDefault));
+        const int k = grp & 1;
+        if (!staged[k]) HCHK(h, hipEventCreateWithFlags(&staged[k], hipEventDisableTiming));
+        else HCHK(h, hipEventSynchronize(staged[k]));
+        std::copy(A.begin(), A.end(), hargs + k * n);
+        HCHK(h, hipMemcpyAsync(dargs + k * n, hargs + k * n, n * sizeof(Args), hipMemcpyHostToDevice, s));
+        HCHK(h, hipEventRecord(staged[k], s));
+        *out = dargs + k * n;
         return LP_PIVOTED;
     }
     Members members(lp_handle *) override { return all; }
@@ -421,23 +438,43 @@ static int alloc_handle(lp_handle *h)
     HCHK(h, hipMalloc(&h->T, tbytes));
     HCHK(h, hipMemsetAsync(h->T, 0, tbytes, h->s));
     h->Tb[0] = h->T;
+    // LPGPU_SWEEP_OOP: 1 always, 0 never, unset: by size (> 512 MiB)
+    static const int oop_env = [] {
+        const char *v = std::getenv("LPGPU_SWEEP_OOP");
+        return v ? std::atoi(v) : 2;
+    }();
     {
         // out-of-place sweeps where the tableau is far beyond the 256 MB
         // Infinity Cache: cfg4 (2.2 GB) 842 -> 812 us per sweep (0.64 -> 0.66
         // of the HBM spec, same box); at cfg3's 273 MB the in-place pass keeps
         // the tableau in the cache for the selection's column reads (OOP:
         // selection 4.47 -> 4.67 us per pivot, 157k -> 152k pivots/s).
-        // LPGPU_SWEEP_OOP: 1 always, 0 never, unset: by size (> 512 MiB)
-        static const int oop_env = [] {
-            const char *v = std::getenv("LPGPU_SWEEP_OOP");
-            return v ? std::atoi(v) : 2;
-        }();
         h->oop = oop_env == 1 || (oop_env == 2 && tbytes > ((size_t)512 << 20));
+        // by size, only where the second buffer fits with room to spare (the
+        // group data below, other handles): a tableau of more than about half
+        // the device stays in place rather than failing to open
+        if (h->oop && oop_env == 2) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+                (void)hipGetLastError();
+                h->oop = false;
+            } else if (fr < tbytes + tbytes / 8 + ((size_t)1 << 30)) {
+                h->oop = false;
+            }
+        }
     }
     if (h->oop) {
         // the second buffer: its padding columns stay 0 like T's (no sweep
-        // writes past column n)
-        HCHK(h, hipMalloc(&h->Tb[1], tbytes));
+        // writes past column n).  Unforced, a failed allocation falls back to
+        // in-place sweeps.
+        if (hipMalloc(&h->Tb[1], tbytes) != hipSuccess) {
+            (void)hipGetLastError();
+            h->Tb[1] = nullptr;
+            if (oop_env == 1) HCHK(h, hipErrorOutOfMemory);
+            h->oop = false;
+        }
+    }
+    if (h->oop) {
         HCHK(h, hipMemsetAsync(h->Tb[1], 0, tbytes, h->s));
         HCHK(h, hipMalloc(&h->dflips, sizeof(unsigned)));
         HCHK(h, hipMemsetAsync(h->dflips, 0, sizeof(unsigned), h->s));
@@ -1030,10 +1067,11 @@ static int enqueue_group(const Members &M, const std::vector<Args> &A, const lpk
     const unsigned next = h0->gseq % ((1u << 23) - 1) + 1;   // the seq launch_group_timed takes
     for (size_t k = 0; k < M.size(); ++k)
         if (M[k]->fault_launch > 0 && (unsigned)M[k]->fault_launch == next) As[k].fault = M[k]->fault_t + 1;
-    CALL(g->stage_args(h0, As));
+    Args *dA = nullptr;
+    CALL(g->stage_args(h0, As, grp, &dA));
     // the members' launch counters advance together (their tags must match)
     for (size_t k = 1; k < M.size(); ++k) M[k]->gseq = next;
-    return launch_group_timed(h0, A[0], geo, grp, cnt, from_erec, xr, g->dargs, (int)M.size(), cs);
+    return launch_group_timed(h0, A[0], geo, grp, cnt, from_erec, xr, dA, (int)M.size(), cs);
 }
 
 // fold the recorded launches into the totals.  Called when the totals are

@@ -55,7 +55,7 @@ namespace {
 #ifdef LPK_STAMPS
 // (the sums are 32-bit and kept in VGPRs -- in SGPRs they pushed the kernel
 // into spilling scalar registers, which distorted what they measured)
-#define SEL_CLK_DECL unsigned clk_[16] = {}; unsigned long long clk_t = __builtin_amdgcn_s_memtime(), clk_r0 = 0;
+#define SEL_CLK_DECL unsigned clk_[20] = {}; unsigned long long clk_t = __builtin_amdgcn_s_memtime(), clk_r0 = 0;
 #define SEL_CLK(k)                                                                \
     do {                                                                          \
         const unsigned long long n_ = __builtin_amdgcn_s_memtime();               \
@@ -243,6 +243,9 @@ __device__ __forceinline__ void row_chain(double (&x)[IPL], const double (&mr)[N
 // immediate offset (the per-granule addresses of the general layout, kept
 // live across the pivot loop, cost k_sel about 70 VGPRs).
 constexpr int SEL_SLOT = 64;
+#ifndef SEL_XS_ROWPF
+#define SEL_XS_ROWPF 1         // XS: the shard's candidate row loaded during the cross-shard exchange
+#endif
 #ifndef SEL_PIPE
 #define SEL_PIPE 0             // exchanges keep two polls in flight
 #endif
@@ -972,6 +975,19 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 for (int r = 0; r < XS_NREP; ++r)
                     st_sc1(&xsum[r * XS_READER_STRIDE + par * 128 + lane * XS_SHARDS + shard], v);
             }
+            // while the shards' summaries travel: the loads of this shard's
+            // candidate row (used as they are if it wins; otherwise they have
+            // brought that row into the Infinity Cache, where the winning
+            // shard's own loads make the other shards' reads of ITS row hits)
+            long long Rpre = NONE;
+#if SEL_XS_ROWPF
+            if constexpr (!XR) {
+                if (R != NONE) {
+                    prow_issue(R);
+                    Rpre = R;
+                }
+            }
+#endif
             unsigned x[SEL_NGX];
             const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
             if (!sel_gather<SEL_NGX, XS_SHARDS>(xsl, XS_SHARDS, gtag(seq, t, 2), x, &ctlv->bar_timeout, spin)) {
@@ -1056,7 +1072,10 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             // every shard: the pivot row on its blocks' columns from the
             // stored row and the leaving row's multipliers (write-through);
             // XR: the device's candidate, computed in the cross-rank step
-            if constexpr (!XR) prow(R, aR);
+            if constexpr (!XR) {
+                if (R != Rpre) prow_issue(R);
+                prow_finish(aR);
+            }
         }
         if constexpr (XR) {
             // ---- leaving row across ranks (as k_group): every rank sends
@@ -1106,12 +1125,14 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 prow(R, aR);
                 send_row(3);
             }
+            SEL_CLK(16);
             unsigned x[SEL_NGX];
             const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
             if (!gather_x<SEL_NGX>(xsl, N, gtag(seq, t, 2), x, &ctlv->bar_timeout, xticks)) {
                 status = LP_DEVICE_ERROR;
                 break;
             }
+            SEL_CLK(14);
             const double lp = lane < N ? mk_d(x[0], x[1]) : INFINITY;
             const double gg = wmin(lp);
             if (!(gg < INFINITY)) {
@@ -1213,6 +1234,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 }
                 if (status != LP_PIVOTED) break;
             }
+            SEL_CLK(17);
             xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
             p0 = bR / aR;
         } else if constexpr (!XS) {
@@ -1395,6 +1417,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     if (A.stamps && lane == 0 && shard == 0) {
         long long *o = A.stamps + BMAX * 16 + (long long)b * 32;
         for (int k = 0; k < 16; ++k) o[k] = (long long)clk_[k];
+        for (int k = 16; k < 20; ++k) o[20 + k - 16] = (long long)clk_[k];   // XR: send, receive
         o[16] = ndone;
         o[17] = (long long)(__builtin_amdgcn_s_memrealtime() - clk_r0);   // 100 MHz ticks of the pivots
         o[18] = (long long)(clk_t - 0);

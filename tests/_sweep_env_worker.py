@@ -1,7 +1,8 @@
-"""Child process of test_gpu_r2.py::test_sweep_grid_modes_bit_exact: the
-sweep's grid switches (LPGPU_SWEEP_TAIL, LPGPU_SWEEP_DP) are read once per
-process, so each setting runs here, over several shapes, against the f64
-oracle.  Prints one line per shape and "ALL OK" at the end."""
+"""Child process of test_gpu_r2.py::test_sweep_grid_modes_bit_exact (and
+test_gpu_r5.py's tail test): the sweep's grid switches (LPGPU_SWEEP_TAIL,
+LPGPU_SWEEP_DP, LPGPU_SWEEP_CUS) are read once per process, so each setting
+runs here, over several shapes (or SWEEP_SHAPES), against the f64 oracle.
+Prints one line per shape and "ALL OK" at the end."""
 import os
 import sys
 
@@ -21,7 +22,11 @@ SHAPES = [("tall", 777, 64, 20, 8), ("mixed", 333, 100, 24, 16), ("tall", 4099, 
 
 
 def main():
-    for kind, m, ns, k, block in SHAPES:
+    shapes = SHAPES
+    if os.environ.get("SWEEP_SHAPES"):           # "kind,m,ns,pivots,block;..."
+        shapes = [(f[0], int(f[1]), int(f[2]), int(f[3]), int(f[4]))
+                  for f in (x.split(",") for x in os.environ["SWEEP_SHAPES"].split(";"))]
+    for kind, m, ns, k, block in shapes:
         T = gen.tableau(kind, m, ns, 11)
         o = F64Tableau(T.copy())
         _, olog = o.run(0, k)

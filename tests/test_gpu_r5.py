@@ -1,0 +1,30 @@
+"""Round 5 GPU tests (MI355X, through the C-ABI):
+
+* the sweep's tail piece of <= 4 columns, rows across
+  lanes, must cover every row of a block's tail, however many -- a tall
+  narrow tableau on a grid sized for 8 CUs (LPGPU_SWEEP_CUS) gives tails of
+  several times 64 W rows per block (8- and 4-wave sweeps, 1 and 3 tail
+  columns), every bit as oracle/lp_f64.c's.
+
+Reference: /root/reference/lpsol/tableau.py:269-280 (rowAdd, the rank-1
+update the sweep applies for every pivot of a group).
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shapes", [
+    "tall,20000,512,100,64",      # 8 waves, 1 tail column, 2504-row tails (64 W = 512)
+    "tall,20000,514,80,64",       # 8 waves, 3 tail columns
+    "tall,9000,256,80,64",        # 4 waves, 1 tail column, 568-row tails (64 W = 256)
+])
+def test_sweep_tail_rows_beyond_one_pass(shapes):
+    worker = os.path.join(os.path.dirname(__file__), "_sweep_env_worker.py")
+    env = dict(os.environ, LPGPU_SWEEP_CUS="8", SWEEP_SHAPES=shapes)
+    run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=280)
+    assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
