@@ -55,7 +55,7 @@ namespace {
 #ifdef LPK_STAMPS
 // (the sums are 32-bit and kept in VGPRs -- in SGPRs they pushed the kernel
 // into spilling scalar registers, which distorted what they measured)
-#define SEL_CLK_DECL unsigned clk_[20] = {}; unsigned long long clk_t = __builtin_amdgcn_s_memtime(), clk_r0 = 0;
+#define SEL_CLK_DECL unsigned clk_[24] = {}; unsigned long long clk_t = __builtin_amdgcn_s_memtime(), clk_r0 = 0;
 #define SEL_CLK(k)                                                                \
     do {                                                                          \
         const unsigned long long n_ = __builtin_amdgcn_s_memtime();               \
@@ -249,6 +249,9 @@ constexpr int SEL_SLOT = 64;
 #ifndef SEL_PIPE
 #define SEL_PIPE 0             // exchanges keep two polls in flight
 #endif
+#ifndef SEL_POLL1
+#define SEL_POLL1 0            // exchanges poll one word of each summary until it arrives
+#endif
 #ifndef SEL_SLEEP
 #define SEL_SLEEP 1            // s_sleep between the polls of an exchange (64 clocks per unit)
 #endif
@@ -262,6 +265,25 @@ __device__ __forceinline__ T vgpr(T x)
     asm("" : "+v"(x));
     return x;
 }
+
+// row r of a row-major array of ldb-byte rows: one 32 x 32 + 64-bit
+// multiply-add (a 64-bit row index times a 64-bit pitch costs four VALU ops
+// on the leaving row's critical path)
+template <typename T>
+__device__ __forceinline__ T *rowp(T *base, long long r, unsigned ldb)
+{
+    return reinterpret_cast<T *>(reinterpret_cast<char *>(base) + (unsigned long long)(unsigned)r * ldb);
+}
+template <typename T>
+__device__ __forceinline__ const T *rowp(const T *base, long long r, unsigned ldb)
+{
+    return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (unsigned long long)(unsigned)r * ldb);
+}
+// a wave's ballot of a condition: the lane mask straight from the compare
+// (HIP's __ballot takes an int, which costs a select and a second compare)
+__device__ __forceinline__ u64 bal(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+// every active lane: the same, against EXEC
+__device__ __forceinline__ bool wall(bool c) { return __builtin_amdgcn_ballot_w64(c) == __builtin_amdgcn_read_exec(); }
 
 // p + byte offset: with p wave-uniform and a 32-bit per-lane offset the
 // access is one global instruction with a scalar base (no per-lane 64-bit
@@ -371,6 +393,26 @@ __device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, u
 {
     if ((int)threadIdx.x < n) stx<FAST>(&region[threadIdx.x * SEL_SLOT + b], ((u64)tag << 32) | w);
 }
+// the per-pivot exchanges' summaries in NR replicas, `stride` granules apart,
+// block b polling replica b % NR: every summary line is then read by 64 / NR
+// blocks per polling round instead of all 64 (the L2 serves one line's
+// requests one after another)
+#ifndef SEL_NREP
+#define SEL_NREP 1
+#endif
+constexpr int SEL_RSTRIDE = 1024;      // ratio summaries: 9 x 64 granules per replica, 2 fit a region
+constexpr int SEL_ESTRIDE = 512;       // row-0 summaries: 8 x 64, 4 fit
+constexpr int SEL_NREP_R = SEL_NREP < 2 ? SEL_NREP : 2;
+constexpr int SEL_NREP_E = SEL_NREP;
+template <bool FAST, int NR>
+__device__ __forceinline__ void sel_put_rep(u64 *region, int stride, unsigned b, unsigned tag, unsigned w, int n)
+{
+    if ((int)threadIdx.x < n) {
+        const u64 v = ((u64)tag << 32) | w;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) stx<FAST>(&region[r * stride + threadIdx.x * SEL_SLOT + b], v);
+    }
+}
 // every block's summary (lane l: block min(l, G - 1)); polls until every
 // granule carries `tag`, bounded by spin_max polls (the host then redoes the
 // group on the per-pivot kernels)
@@ -388,7 +430,7 @@ __device__ bool sel_gather(const u64 *base, unsigned G, unsigned tag, unsigned (
             w[g] = (unsigned)v;
             ok = ok && (unsigned)(v >> 32) == tag;
         }
-        if (__all(ok)) return true;
+        if (wall(ok)) return true;
         if (spins > spin_max) {
             st_sc1(timeout_flag, 1u);
             return false;
@@ -415,9 +457,9 @@ __device__ __forceinline__ void sel_summary(const double (&vv)[IPL], const doubl
     const double ethr = tie_band(el, tol.cost_tie);
 #pragma unroll
     for (int k = 0; k < IPL; ++k) {
-        const u64 mn = __ballot(vv[k] < -tol.cost);
+        const u64 mn = bal(vv[k] < -tol.cost);
         if (mn && efn == NONE) efn = jc0 + k * 64 + __builtin_ctzll(mn);
-        const u64 mb = __ballot(el < INFINITY && vv[k] <= ethr);
+        const u64 mb = el < INFINITY ? bal(vv[k] <= ethr) : 0ull;   // (direct compares: no select + recompare)
         if (mb && ei == NONE) {
             const int f = __builtin_ctzll(mb);
             ei = jc0 + k * 64 + f;
@@ -462,7 +504,7 @@ struct SelPoll {
             w[g] = (unsigned)d[g];
             ok = ok && (unsigned)(d[g] >> 32) == tag;
         }
-        return __all(ok);
+        return wall(ok);
     }
     __device__ __forceinline__ void issue(const u64 *base, unsigned G)
     {
@@ -490,6 +532,29 @@ struct SelPoll {
                 st_sc1(timeout_flag, 1u);
                 return false;
             }
+        }
+#elif SEL_POLL1
+        // the first load of every summary word is out (issue()); then poll
+        // only the last word of every block until all carry the tag (one
+        // 512-byte load per round instead of NG: the 64 pollers' rounds cost
+        // the XCD's L2 a ninth), read the other words once and check them
+        for (unsigned spins = 0;; ++spins) {
+            if (take(tag, v, w)) return true;
+            if (spins > spin_max) {
+                st_sc1(timeout_flag, 1u);
+                return false;
+            }
+            bool last = (unsigned)(v[NG - 1] >> 32) == tag;
+            while (!wall(last)) {
+                if (++spins > spin_max) {
+                    st_sc1(timeout_flag, 1u);
+                    return false;
+                }
+                __builtin_amdgcn_s_sleep(SEL_SLEEP);
+                v[NG - 1] = ld_sc1(p + (NG - 1) * SEL_SLOT);
+                last = (unsigned)(v[NG - 1] >> 32) == tag;
+            }
+            load(v);
         }
 #else
         for (unsigned spins = 0;; ++spins) {
@@ -570,6 +635,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     double *const Pb = A.P;
     double *const Mb = A.M;
     const long long ld = vgpr(A.ld);
+    const unsigned ldb = vgpr((unsigned)(A.ld * 8));       // bytes per row (host: ld * 8 < 2^32)
     double *const MQv = vgpr(A.MQ);
     double *const row0v = vgpr(A.row0);
     double *const col0v = vgpr(A.col0);
@@ -798,11 +864,12 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         bool okq;
         const double q = row_ratio(a, lcv, tol, okq);
         okq = okq && own;
-        const double lb = wmin(okq ? q : INFINITY);
+        const double qq = okq ? q : INFINITY;
+        const double lb = wmin(qq);
         long long ib = NONE;
         double ab = 0.0, bb = 0.0, qb = 0.0;
         if (lb < INFINITY) {
-            const u64 mask = __ballot(okq && q <= tie_band(lb, tol.ratio_tie));
+            const u64 mask = bal(qq <= tie_band(lb, tol.ratio_tie));   // (the band is finite)
             const int f = __builtin_ctzll(mask);
             ib = lr0 + f;
             ab = rl_d(lo32(a), hi32(a), f);
@@ -825,7 +892,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             wv = wl(wv, hi32(bb), 6);
             wv = wl(wv, lo32(qb), 7);
             wv = wl(wv, hi32(qb), 8);
-            sel_put<FAST>(grR, b, gtag(seq, t, 0), wv, SEL_NGR);
+            sel_put_rep<FAST, SEL_NREP_R>(grR, SEL_RSTRIDE, b, gtag(seq, t, 0), wv, SEL_NGR);
         }
         SEL_EV(2);
         SEL_CLK(5);
@@ -833,7 +900,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         //      travel) the multiplier into its register and to memory
         unsigned w[SEL_NGR];
         SelPoll<SEL_NGR> pr;
-        pr.issue(grR, G);
+        pr.issue(grR + (b % SEL_NREP_R) * SEL_RSTRIDE, G);
         apend = a;
         if (b == 0 && lane == 0) {            // read after the launch only (after the publication:
             *gp(&ctlv->c) = C - 1;            // stores pending at a drain delay the summary)
@@ -859,10 +926,10 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         double px[IPL], pmr[NK];
         int psst = -1;
         auto prow_issue = [&](long long Rl) {
-            const u64 rp = __ballot(lane < t && sRv == Rl);
+            const u64 rp = bal(sRv == Rl);                          // (lanes >= t hold -1)
             psst = rp ? 63 - __builtin_clzll(rp) : -1;             // uniform
             // every load issued before any select (see the column's)
-            const double *const xr = Tb + Rl * ld;                 // wave-uniform
+            const double *const xr = rowp(Tb, Rl, ldb);            // wave-uniform
             const double *const mrp = Mb + Rl;
 #pragma unroll
             for (int k = 0; k < IPL; ++k) px[k] = *gp(at(xr, xoff[k]));
@@ -909,9 +976,11 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         };
         const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
         const double g = wmin(rl);
+        SEL_DONE(g);
+        SEL_CLK(20);
         if (g < INFINITY) {
             const double thr = tie_band(g, tol.ratio_tie);
-            const int bs = __builtin_ctzll(__ballot((unsigned)lane < G && rl <= thr));
+            const int bs = __builtin_ctzll(bal(rl <= thr));         // (lanes >= G: rl = inf, thr finite)
             // (block bs has a candidate: its minimum is finite)
             const long long Rc = un_idx(rl32(w[2], bs));
             if constexpr (!XR && !XS) prow_issue(Rc);
@@ -925,7 +994,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 // candidate; it answers with that row (one more hand-off)
                 const unsigned stag = gtag(seq, t, 4);
                 if (b == (unsigned)bs) {
-                    const int f = __builtin_ctzll(__ballot(okq && q <= thr));
+                    const int f = __builtin_ctzll(bal(okq && q <= thr));
                     const double af = rl_d(lo32(a), hi32(a), f), bf = rl_d(lo32(lcv), hi32(lcv), f);
                     unsigned wv = (unsigned)(lr0 + f);
                     wv = wl(wv, lo32(af), 1);
@@ -1006,7 +1075,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             }
             const double thr = tie_band(gg, tol.ratio_tie);
             if (gg < INFINITY) {
-            const int ps = __builtin_ctzll(__ballot(lane < XS_SHARDS && lp <= thr));
+            const int ps = __builtin_ctzll(bal(lp <= thr));         // (lanes >= XS_SHARDS: inf)
             double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
             bool okp;
             const double qs = row_ratio(as, bs, tol, okp);
@@ -1019,7 +1088,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 // rescan slots), its block 0 publishes the lowest to all
                 u64 *const xst = xsum + XS_RD(shard) * XS_READER_STRIDE + 256 + par * 8;
                 if ((int)shard == ps) {
-                    const u64 mk = __ballot(okq && q <= thr);
+                    const u64 mk = bal(okq && q <= thr);
                     const int fr = mk ? __builtin_ctzll(mk) : 0;
                     const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
                     u64 *const loc = grS + 1024;
@@ -1036,7 +1105,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                         status = LP_DEVICE_ERROR;
                         break;
                     }
-                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
+                    const int bf = __builtin_ctzll(bal((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
                     if (b == 0 && lane < SEL_NGS) {
                         unsigned wv = rl32(wlo[0][0], bf) - 1u;
                         wv = wl(wv, rl32(wlo[0][1], bf), 1);
@@ -1140,7 +1209,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 break;
             }
             const double thr = tie_band(gg, tol.ratio_tie);
-            const int ps = __builtin_ctzll(__ballot(lane < N && lp <= thr));
+            const int ps = __builtin_ctzll(bal(lp <= thr));         // (lanes >= N: inf)
             double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
             bool okp;
             const double qs = row_ratio(as, bs, tol, okp);
@@ -1155,9 +1224,9 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 // that row's normalised values instead of its candidate's
                 // (XS: the rank's first shard whose minimum lies inside the
                 // band holds that row: its blocks offer, its block 0 sends)
-                const int sfirst = XS ? __builtin_ctzll(__ballot(lane < XS_SHARDS && lps <= thr) | (1ull << 63)) : 0;
+                const int sfirst = XS ? __builtin_ctzll(bal(lane < XS_SHARDS && lps <= thr) | (1ull << 63)) : 0;
                 if (A.rank == ps && (int)shard == sfirst) {
-                    const u64 mk = __ballot(okq && q <= thr);
+                    const u64 mk = bal(okq && q <= thr);
                     const int fr = mk ? __builtin_ctzll(mk) : 0;
                     const double ar = rl_d(lo32(a), hi32(a), fr), br = rl_d(lo32(lcv), hi32(lcv), fr);
                     u64 *loc = XS ? grS + 1536 : xbufv + XS_PROW + 2LL * N * XS_PROW_RANK;
@@ -1174,7 +1243,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                         status = LP_DEVICE_ERROR;
                         break;
                     }
-                    const int bf = __builtin_ctzll(__ballot((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
+                    const int bf = __builtin_ctzll(bal((unsigned)lane < G && wlo[0][0] != 0x7fffffffu));
                     const unsigned r0w = rl32(wlo[0][0], bf), a0 = rl32(wlo[0][1], bf), a1 = rl32(wlo[0][2], bf),
                                    b0 = rl32(wlo[0][3], bf), b1 = rl32(wlo[0][4], bf);
                     if (b == 0 && lane < SEL_NGS) {
@@ -1224,7 +1293,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                         pv[k] = mk_d((unsigned)lo, (unsigned)hi);
                         ok = ok && (!cok[k] || ((unsigned)(lo >> 32) == tg && (unsigned)(hi >> 32) == tg));
                     }
-                    if (__all(ok)) break;
+                    if (wall(ok)) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > xticks) {
                         st_sc1(&ctlv->bar_timeout, 1u);
                         status = LP_DEVICE_ERROR;
@@ -1245,7 +1314,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         //      summary; pivot t + 1 gets P[t][C] with the row-0 summaries);
         //      row 0 is stored once, at the end of the launch
         {
-            double *const pt = Pb + (long long)t * ld;          // wave-uniform
+            double *const pt = rowp(Pb, t, ldb);               // wave-uniform
 #pragma unroll
             for (int k = 0; k < IPL; ++k)
                 if (cok[k]) stx<FAST>(at(pt, xoff[k]), pv[k]);
@@ -1262,16 +1331,18 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         double el, eq, epc;
         long long ei, efn;
         sel_summary<IPL>(vv, pv, vmn, jc0, tol, el, ei, eq, epc, efn);
+        SEL_DONE(epc);
+        SEL_CLK(21);
         const bool more = t + 1 < count;
         const unsigned etag = gtag(seq, t, 1);
-        if (more) sel_put<FAST>(grE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
+        if (more) sel_put_rep<FAST, SEL_NREP_E>(grE, SEL_ESTRIDE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
         SEL_EV(4);
         SEL_CLK(11);
         // ---- while the summaries travel: the pivot-row values into LDS,
         //      column 0 of the own rows (this pivot's multiplier is a), the
         //      pivot row's register state, the stall bookkeeping, records
         SelPoll<SEL_NGE> pe;
-        if (more) pe.issue(grE, G);
+        if (more) pe.issue(grE + (b % SEL_NREP_E) * SEL_ESTRIDE, G);
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             if (cok[k]) lP[kc[k] * CS + t] = pv[k];
@@ -1281,7 +1352,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         zpend = li == R;                      // that lane only: its row is P[t] from now on
         if (zpend) {
             pstar = t;
-            arow = Pb + (long long)t * ld;
+            arow = rowp(Pb, t, ldb);
         }
         if (lane == t) sRv = R;
         // stall bookkeeping (simplex.py:132-137), min-index switch
@@ -1349,9 +1420,11 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 if (Cn != NONE) owner = (int)((Cn - 1) / cpb);
             } else {
                 const double g2 = wmin(el2);
+                SEL_DONE(g2);
+                SEL_CLK(18);
                 if (g2 < -tol.cost) {
                     ethr = tie_band(g2, tol.cost_tie);
-                    const int bs = __builtin_ctzll(__ballot(in && el2 <= ethr));
+                    const int bs = __builtin_ctzll(bal(el2 <= ethr));   // (lanes >= G: inf)
                     const double qs = rl_d(we[2], we[3], bs);
                     if (qs <= ethr) {
                         Cn = un_idx(rl32(we[4], bs));
@@ -1373,7 +1446,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                         bool found = false;
 #pragma unroll
                         for (int k = 0; k < IPL; ++k) {
-                            const u64 mk = __ballot(cok[k] && vn[k] <= ethr);
+                            const u64 mk = bal(cok[k] && vn[k] <= ethr);
                             if (!found && mk) {
                                 found = true;
                                 kf = k;
@@ -1409,6 +1482,8 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 pcw = rl_d(y[3], y[4], 0);
             }
             C = Cn;
+            SEL_DONE(pcw);
+            SEL_CLK(19);
             if (C == NONE) status = stop ? LP_OBJ_INCREASED : capped ? LP_CAP_REACHED : LP_OPTIMAL;
         }
         SEL_CLK(0);
@@ -1417,7 +1492,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     if (A.stamps && lane == 0 && shard == 0) {
         long long *o = A.stamps + BMAX * 16 + (long long)b * 32;
         for (int k = 0; k < 16; ++k) o[k] = (long long)clk_[k];
-        for (int k = 16; k < 20; ++k) o[20 + k - 16] = (long long)clk_[k];   // XR: send, receive
+        for (int k = 16; k < 24; ++k) o[20 + k - 16] = (long long)clk_[k];   // XR, sub-phases
         o[16] = ndone;
         o[17] = (long long)(__builtin_amdgcn_s_memrealtime() - clk_r0);   // 100 MHz ticks of the pivots
         o[18] = (long long)(clk_t - 0);
@@ -1519,7 +1594,7 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             return;
         }
         const bool same = !((unsigned)lane < G) || wx[0] == me;
-        if (!__all(same)) {
+        if (!wall(same)) {
             if (b == 0 && lane == 0) {
                 *gp(&ctl->sel_flags) = 8u | 4u;
                 st_sc1(&ctl->bar_timeout, 1u);

@@ -17,14 +17,15 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "linear-program-solver_amd"))
 
-NAMES = {1: "issue", 2: "colload", 3: "colchain", 4: "ratio", 5: "rpub", 6: "rgather", 7: "leave",
-         8: "rowload", 9: "rowchain", 10: "div", 16: "xsend", 14: "xshard/xgather", 17: "xrecv",
-         11: "rowfin+epub", 12: "tail", 13: "egather", 0: "decide"}
-ORDER = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 16, 14, 17, 11, 12, 13, 0]
+NAMES = {1: "issue", 2: "colload", 3: "colchain", 4: "ratio", 5: "rpub", 6: "rgather", 20: "leave:wmin",
+         7: "leave:rest", 8: "rowload", 9: "rowchain", 10: "div", 16: "xsend", 14: "xshard/xgather", 17: "xrecv",
+         21: "rowfin:summary", 11: "rowfin:rest+epub", 12: "tail", 13: "egather", 18: "decide:wmin",
+         19: "decide:pick", 0: "decide:rest"}
+ORDER = [1, 2, 3, 4, 5, 6, 20, 7, 8, 9, 10, 16, 14, 17, 21, 11, 12, 13, 18, 19, 0]
 
 
 def clk(o, k):
-    # select.hip: phases 0..15 at o[0..15], 16..19 at o[20..23]
+    # select.hip: phases 0..15 at o[0..15], 16..23 at o[20..27]
     return o[k] if k < 16 else o[20 + k - 16]
 
 
@@ -37,7 +38,7 @@ def report(buf, G, blk):
         if nd <= 1:
             continue
         # phase 0 and 12/13 run nd - 1 times (no next pivot after the last)
-        per.append({k: clk(o, k) / (nd - 1 if k in (0, 12, 13) else nd) for k in ORDER})
+        per.append({k: clk(o, k) / (nd - 1 if k in (0, 12, 13, 18, 19) else nd) for k in ORDER})
         if o[17] > 0:
             ghz_s.append(sum(clk(o, k) for k in ORDER) / (o[17] * 10.0))   # cycles per ns -> GHz
     ghz = sorted(ghz_s)[len(ghz_s) // 2] if ghz_s else 2.1
@@ -46,7 +47,7 @@ def report(buf, G, blk):
     for k in ORDER:
         v = [p[k] for p in per]
         mean = sum(v) / len(v)
-        if mean == 0 and k in (14, 16, 17):
+        if mean == 0 and k in (14, 16, 17, 18, 19, 20, 21):
             continue
         tot += mean
         print(f"{NAMES[k]:>14s}  mean {mean:7.0f} cyc {mean / ghz / 1000:5.2f} us   max {max(v):7.0f}   "
