@@ -449,22 +449,42 @@ __device__ __forceinline__ void sel_summary(const double (&vv)[IPL], const doubl
                                             long long jc0, const lp_tol &tol, double &el, long long &ei,
                                             double &eq, double &epc, long long &efn)
 {
+    // (branch-free: every ballot, then the first k with a hit picked by
+    // scalar selects; the readlanes of each k issue together)
+    u64 mn[IPL];
+#pragma unroll
+    for (int k = 0; k < IPL; ++k) mn[k] = bal(vv[k] < -tol.cost);   // independent of the minimum
     el = wmin(vmin_);
+    const double ethr = tie_band(el, tol.cost_tie);
     efn = NONE;
+#pragma unroll
+    for (int k = IPL - 1; k >= 0; --k)
+        if (mn[k]) efn = jc0 + k * 64 + __builtin_ctzll(mn[k]);
     ei = NONE;
     eq = 0.0;
     epc = 0.0;
-    const double ethr = tie_band(el, tol.cost_tie);
+    if (el < INFINITY) {
+        u64 mb[IPL];
 #pragma unroll
-    for (int k = 0; k < IPL; ++k) {
-        const u64 mn = bal(vv[k] < -tol.cost);
-        if (mn && efn == NONE) efn = jc0 + k * 64 + __builtin_ctzll(mn);
-        const u64 mb = el < INFINITY ? bal(vv[k] <= ethr) : 0ull;   // (direct compares: no select + recompare)
-        if (mb && ei == NONE) {
-            const int f = __builtin_ctzll(mb);
-            ei = jc0 + k * 64 + f;
-            eq = rl_d(lo32(vv[k]), hi32(vv[k]), f);
-            epc = rl_d(lo32(pv[k]), hi32(pv[k]), f);
+        for (int k = 0; k < IPL; ++k) mb[k] = bal(vv[k] <= ethr);   // (direct compares: no select + recompare)
+        int kf = IPL, f = 0;
+#pragma unroll
+        for (int k = IPL - 1; k >= 0; --k)
+            if (mb[k]) {
+                kf = k;
+                f = __builtin_ctzll(mb[k]);
+            }
+        if (kf < IPL) {
+            ei = jc0 + kf * 64 + f;
+            double q1 = 0.0, p1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) {
+                const double qk = rl_d(lo32(vv[k]), hi32(vv[k]), f), pk = rl_d(lo32(pv[k]), hi32(pv[k]), f);
+                q1 = k == kf ? qk : q1;
+                p1 = k == kf ? pk : p1;
+            }
+            eq = q1;
+            epc = p1;
         }
     }
 }
@@ -1403,11 +1423,17 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         }
         SEL_CLK(13);
         SEL_EV(5);
-        rule = __builtin_amdgcn_readfirstlane(rule);
-        stop = __builtin_amdgcn_readfirstlane(stop);
         {
+            // the standard rule's minimum first, unconditionally: the loop's
+            // bookkeeping below fills its dependency gaps (behind the rule and
+            // stop branches it ran after them)
             const bool in = (unsigned)lane < G;
             const double el2 = in ? mk_d(we[0], we[1]) : INFINITY;
+            const double g2 = wmin(el2);
+            SEL_DONE(g2);
+            SEL_CLK(18);
+            rule = __builtin_amdgcn_readfirstlane(rule);
+            stop = __builtin_amdgcn_readfirstlane(stop);
             const long long ef2 = in ? un_idx(we[5]) : NONE;
             const bool capped = cap >= 0 && npiv >= cap;
             long long Cn = NONE;
@@ -1419,17 +1445,17 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 Cn = wave_min_ll(ef2);
                 if (Cn != NONE) owner = (int)((Cn - 1) / cpb);
             } else {
-                const double g2 = wmin(el2);
-                SEL_DONE(g2);
-                SEL_CLK(18);
                 if (g2 < -tol.cost) {
                     ethr = tie_band(g2, tol.cost_tie);
                     const int bs = __builtin_ctzll(bal(el2 <= ethr));   // (lanes >= G: inf)
+                    // (every readlane at once, then the check)
                     const double qs = rl_d(we[2], we[3], bs);
+                    const long long cb = un_idx(rl32(we[4], bs));
+                    const double pb = rl_d(we[6], we[7], bs);
                     if (qs <= ethr) {
-                        Cn = un_idx(rl32(we[4], bs));
+                        Cn = cb;
                         f0 = qs;
-                        pcw = rl_d(we[6], we[7], bs);
+                        pcw = pb;
                     } else {
                         owner = bs;           // rare: the first column of its slice inside the band
                     }
