@@ -65,6 +65,9 @@ WORKLOADS = {
     # one-XCD cross-rank kernel k_sel<XR>, G = 64) with two ranks on ONE GPU:
     # 6144 columns, so both ranks' launches are resident at once
     "cfg4r8": ("tall", 8192, 6144, "8192x6144 G_tall seed 3: two 4096-row ranks (the 8-GPU cfg4 rank geometry)"),
+    # one such rank's shape alone on one GPU (no cross-rank exchange): the
+    # baseline the rehearsal's XR overhead is measured against
+    "cfg4r8one": ("tall", 4096, 6144, "4096x6144 G_tall seed 3: one cfg4r8 rank's shape on one GPU"),
 }
 
 

@@ -279,6 +279,14 @@ __device__ __forceinline__ const T *rowp(const T *base, long long r, unsigned ld
 {
     return reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + (unsigned long long)(unsigned)r * ldb);
 }
+// all N values materialised at this point (and none sunk into a branch)
+template <int N>
+__device__ __forceinline__ void keep_all(double (&v)[N])
+{
+    if constexpr (N == 1) asm("" : "+v"(v[0]));
+    else if constexpr (N == 2) asm("" : "+v"(v[0]), "+v"(v[1]));
+    else asm("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+}
 // a wave's ballot of a condition: the lane mask straight from the compare
 // (HIP's __ballot takes an int, which costs a select and a second compare)
 __device__ __forceinline__ u64 bal(bool c) { return __builtin_amdgcn_ballot_w64(c); }
@@ -736,6 +744,14 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     Ctl *const ctlv = vgpr(ctl);            // the loop's hand-off flags and records
     u64 *const xbufv = vgpr(A.xbuf);        // XR: this rank's exchange buffer, the peers'
     unsigned long long *const *const peerv = vgpr(A.peer);
+    // XR: lane p (< nranks) holds peer p's exchange buffer address (a load
+    // per peer and pivot was a dependent memory round trip ahead of the sends)
+    u64 peerl = 0;
+    if constexpr (XR) peerl = lane < A.nranks ? (u64)*gp(peerv + lane) : 0ull;
+    auto peer = [&](int p) -> u64 * {
+        return reinterpret_cast<u64 *>(((u64)__builtin_amdgcn_readlane((unsigned)(peerl >> 32), p) << 32) |
+                                       (u64)(unsigned)__builtin_amdgcn_readlane((unsigned)peerl, p));
+    };
     const long long rbv = vgpr(A.rb);
     double z0 = 0.0;
     if (reset) {
@@ -979,14 +995,16 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             row_chain<IPL, NB>(x, mr, lP, kc, t);
             SEL_DONE(x[IPL - 1]);
             SEL_CLK(9);
-            // every lane divides (the IPL divisions interleave; a branch
-            // around each made them run one after another), then selects
+            // every lane divides, then selects: one barrier over all IPL
+            // quotients, so that their division sequences interleave (a
+            // branch around each, or a barrier per quotient, ran them one
+            // after another)
+            double qd[IPL];
 #pragma unroll
-            for (int k = 0; k < IPL; ++k) {
-                double qd = x[k] / avv;
-                asm("" : "+v"(qd));
-                pv[k] = (jk[k] == C) ? 1.0 : qd;
-            }
+            for (int k = 0; k < IPL; ++k) qd[k] = x[k] / avv;
+            keep_all<IPL>(qd);
+#pragma unroll
+            for (int k = 0; k < IPL; ++k) pv[k] = (jk[k] == C) ? 1.0 : qd[k];
             SEL_DONE(pv[IPL - 1]);
             SEL_CLK(10);
         };
@@ -1003,7 +1021,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             const int bs = __builtin_ctzll(bal(rl <= thr));         // (lanes >= G: rl = inf, thr finite)
             // (block bs has a candidate: its minimum is finite)
             const long long Rc = un_idx(rl32(w[2], bs));
-            if constexpr (!XR && !XS) prow_issue(Rc);
+            if constexpr (!XS) prow_issue(Rc);
             aR = rl_d(w[3], w[4], bs);
             bR = rl_d(w[5], w[6], bs);
             const double qR = rl_d(w[7], w[8], bs);
@@ -1031,7 +1049,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 R = (long long)rl32(y[0], 0);
                 aR = rl_d(y[1], y[2], 0);
                 bR = rl_d(y[3], y[4], 0);
-                if constexpr (!XR && !XS) prow_issue(R);
+                if constexpr (!XS) prow_issue(R);
             }
         } else if (!XR && !XS) {
             status = LP_UNBOUNDED;
@@ -1191,14 +1209,14 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 for (int p = 0; p < N; ++p)
 #pragma unroll
                     for (int r = 0; r < NREP; ++r)
-                        st_sys(&(*gp(peerv + p))[r * XS_XREP + par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
+                        st_sys(&peer(p)[r * XS_XREP + par * XS_SUM_PAR + A.rank * 8 + lane], tg | wv);
             }
             auto send_row = [&](int ph) {
                 const unsigned long long tg = (u64)gtag(seq, t, ph) << 32;
                 for (int p = 0; p < N; ++p) {
                     if (p == A.rank) continue;
                     if (XS && ((p - A.rank + N) % N - 1) % XS_SHARDS != (int)shard) continue;
-                    u64 *dst = (*gp(peerv + p)) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
+                    u64 *dst = peer(p) + XS_PROW + (long long)(par * N + A.rank) * XS_PROW_RANK +
                                (long long)b * XS_PROW_BLOCK;
 #pragma unroll
                     for (int k = 0; k < IPL; ++k) {
@@ -1211,7 +1229,9 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 }
             };
             if (R != NONE) {
-                prow(R, aR);
+                // (one XCD: the loads were issued at the rank's decision)
+                if constexpr (XS) prow(R, aR);
+                else prow_finish(aR);
                 send_row(3);
             }
             SEL_CLK(16);
@@ -1275,7 +1295,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                         for (int p = 0; p < N; ++p)
 #pragma unroll
                             for (int r = 0; r < NREP; ++r)
-                                st_sys(&(*gp(peerv + p))[r * XS_XREP + par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
+                                st_sys(&peer(p)[r * XS_XREP + par * XS_SUM_PAR + NRANK_MAX * 8 + lane],
                                        ((u64)gtag(seq, t, 5) << 32) | wv);
                     }
                 }
@@ -1298,6 +1318,9 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             R = win ? rg - rbv + 1 : -1;
             aR = as;
             bR = bs;
+            // column 0's pivot value now, while the winner's row travels
+            p0 = bR / aR;
+            asm volatile("" : "+v"(p0));
             if (!win) {
                 // the winning rank's block b sent these columns
                 const u64 *src = xbufv + XS_PROW + (long long)(par * N + ps) * XS_PROW_RANK +
@@ -1325,7 +1348,6 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             }
             SEL_CLK(17);
             xwait = vgpr(xwait + (__builtin_amdgcn_s_memrealtime() - xw0));
-            p0 = bR / aR;
         } else if constexpr (!XS) {
             prow_finish(aR);                  // (loads issued at the decision)
         }
