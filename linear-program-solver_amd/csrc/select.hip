@@ -73,7 +73,7 @@ namespace {
 // 5 every row-0 summary seen
 #define SEL_EV(k)                                                                                   \
     do {                                                                                            \
-        if (A.stamps && lane == 0 && t < 48 && shard == 0)                                          \
+        if (A.stamps && lane == 0 && t < 48 && shard == 0 && b < 64)                                \
             *gp(A.stamps + BMAX * 16 + 4096 + ((long long)t * 64 + b) * 8 + (k)) =                  \
                 (long long)__builtin_amdgcn_s_memrealtime();                                        \
     } while (0)
@@ -249,6 +249,9 @@ constexpr int SEL_SLOT = 64;
 #ifndef SEL_PIPE
 #define SEL_PIPE 0             // exchanges keep two polls in flight
 #endif
+#ifndef SEL_W2_DEFAULT
+#define SEL_W2_DEFAULT 0       // the 128-block one-column-per-lane form by default (sel_geom)
+#endif
 #ifndef SEL_POLL1
 #define SEL_POLL1 0            // exchanges poll one word of each summary until it arrives
 #endif
@@ -396,10 +399,10 @@ __device__ __forceinline__ unsigned wl_(unsigned w, unsigned v)
 #define wl(W, V, L) wl_<L>((W), (V))
 
 // the words of a summary: lane g (< n) stores word g of block b
-template <bool FAST>
+template <bool FAST, int SLOT = SEL_SLOT>
 __device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, unsigned w, int n)
 {
-    if ((int)threadIdx.x < n) stx<FAST>(&region[threadIdx.x * SEL_SLOT + b], ((u64)tag << 32) | w);
+    if ((int)threadIdx.x < n) stx<FAST>(&region[threadIdx.x * SLOT + b], ((u64)tag << 32) | w);
 }
 // the per-pivot exchanges' summaries in NR replicas, `stride` granules apart,
 // block b polling replica b % NR: every summary line is then read by 64 / NR
@@ -512,7 +515,7 @@ __device__ __forceinline__ unsigned esum_words(double el, double eq, long long e
 // sel_gather split in two: issue() sends the first polls, finish() checks them
 // (and polls on); work placed between the two runs while the polls are in
 // flight (the scheduling barriers keep the loads ahead of it)
-template <int NG>
+template <int NG, int STRIDE = SEL_SLOT>
 struct SelPoll {
     const u64 *p;
     u64 v[NG];
@@ -522,7 +525,7 @@ struct SelPoll {
     __device__ __forceinline__ void load(u64 (&d)[NG])
     {
 #pragma unroll
-        for (int g = 0; g < NG; ++g) d[g] = ld_sc1(p + g * SEL_SLOT);
+        for (int g = 0; g < NG; ++g) d[g] = ld_sc1(p + g * STRIDE);
     }
     __device__ __forceinline__ bool take(unsigned tag, const u64 (&d)[NG], unsigned (&w)[NG])
     {
@@ -579,7 +582,7 @@ struct SelPoll {
                     return false;
                 }
                 __builtin_amdgcn_s_sleep(SEL_SLEEP);
-                v[NG - 1] = ld_sc1(p + (NG - 1) * SEL_SLOT);
+                v[NG - 1] = ld_sc1(p + (NG - 1) * STRIDE);
                 last = (unsigned)(v[NG - 1] >> 32) == tag;
             }
             load(v);
@@ -643,13 +646,19 @@ constexpr int XS_NREP = XS_SHARDS;
 // every shard forms the winner's pivot row itself from the shared tableau (the
 // multipliers are stored write-through for that) -- no row travels.
 // first: as k_group's (call start: reset / eager / enter).
-template <int IPL, int NB, bool XR, bool FAST, bool XS>
+// W2 (one XCD, single device): 128 blocks of one column per lane (the row
+// chain, the division and the row-0 summary per pivot halve), blocks 0..63
+// own the rows as before; the row-0 summaries are 128 (lane l holds blocks l
+// and l + 64), the ratio summaries 64 (the row blocks').
+template <int IPL, int NB, bool XR, bool FAST, bool XS, bool W2 = false>
 __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const unsigned G, int grp, int count,
                                          int from_erec, unsigned seq, int first, int fmode, long long fcap,
                                          double *lP, long long npiv, long long nstd, long long stuck, int rule,
                                          const unsigned shard)
 {
     constexpr int CS = NB + 2;             // LDS stride of a column's pivot values (16-B reads, no conflicts)
+    constexpr int NRE = W2 ? 2 : 1;        // row-0 summaries per lane (blocks lane + 64 k)
+    constexpr int SLOTE = W2 ? 128 : SEL_SLOT;   // granules between granule g and g + 1 of the row-0 region
     constexpr int NK = NB / 16;            // broadcast registers
     const int lane = threadIdx.x;
     Ctl *ctl = A.ctl;
@@ -680,7 +689,9 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     // block's share of the variable columns 1..n (column 0 is every block's)
     const long long rps = XS ? (A.rc + XS_SHARDS - 1) / XS_SHARDS : A.rc;   // rows of a shard
     const long long rs0 = XS ? (long long)shard * rps : 0;                   // its first (0-based)
-    const long long rpb = (rps + G - 1) / G;
+    static_assert(!W2 || (!XR && !XS && IPL == 1), "k_sel<W2>: one XCD, single device, one column per lane");
+    const unsigned GR = W2 ? G / 2 : G;    // blocks that own rows (and publish ratio summaries)
+    const long long rpb = (rps + GR - 1) / GR;
     const long long lr0 = vgpr(1 + rs0 + (long long)b * rpb),
                     lr1 = vgpr(min(1 + rs0 + min((long long)b * rpb + rpb, rps), A.rows));
     const long long li = lr0 + lane;
@@ -800,15 +811,26 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         if (!from_erec && !enter) {
             C = ld_sc1(&ctl->c) + 1;
         } else {
-            double el = INFINITY, eq = 0.0;
-            long long ei = NONE, ef = NONE;
-            const bool in = (unsigned)lane < G;
+            // (W2: two summaries per lane, blocks lane and lane + 64)
+            double el[NRE], eq[NRE];
+            long long ei[NRE], ef[NRE];
+#pragma unroll
+            for (int k = 0; k < NRE; ++k) {
+                el[k] = INFINITY;
+                eq[k] = 0.0;
+                ei[k] = NONE;
+                ef[k] = NONE;
+            }
             if (from_erec) {
-                if (in) {
-                    el = ld_sc1(&erecv[lane].l);
-                    ei = ld_sc1(&erecv[lane].i);
-                    eq = ld_sc1(&erecv[lane].q);
-                    ef = ld_sc1(&erecv[lane].fneg);
+#pragma unroll
+                for (int k = 0; k < NRE; ++k) {
+                    const unsigned bk = lane + 64 * k;
+                    if (bk < G) {
+                        el[k] = ld_sc1(&erecv[bk].l);
+                        ei[k] = ld_sc1(&erecv[bk].i);
+                        eq[k] = ld_sc1(&erecv[bk].q);
+                        ef[k] = ld_sc1(&erecv[bk].fneg);
+                    }
                 }
             } else {
                 double vv[IPL], vmn = INFINITY, pz[IPL];
@@ -823,27 +845,36 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 sel_summary<IPL>(vv, pz, vmn, jc0, tol, sel_, sei_, seq_, spc_, sfn_);
                 const unsigned etag = gtag(seq, 0, 0);
                 drain_stores();
-                sel_put<FAST>(grE, b, etag, esum_words(sel_, seq_, sei_, sfn_, spc_), SEL_NGE);
-                unsigned w[SEL_NGE];
-                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctlv->bar_timeout, spin)) status = LP_DEVICE_ERROR;
-                if (in) {
-                    el = mk_d(w[0], w[1]);
-                    eq = mk_d(w[2], w[3]);
-                    ei = un_idx(w[4]);
-                    ef = un_idx(w[5]);
+                sel_put<FAST, SLOTE>(grE, b, etag, esum_words(sel_, seq_, sei_, sfn_, spc_), SEL_NGE);
+#pragma unroll
+                for (int k = 0; k < NRE; ++k) {
+                    unsigned w[SEL_NGE];
+                    const unsigned gk = min(64u, G - 64u * k);
+                    if (!sel_gather<SEL_NGE, SLOTE>(grE + 64 * k, gk, etag, w, &ctlv->bar_timeout, spin))
+                        status = LP_DEVICE_ERROR;
+                    if ((unsigned)lane < gk) {
+                        el[k] = mk_d(w[0], w[1]);
+                        eq[k] = mk_d(w[2], w[3]);
+                        ei[k] = un_idx(w[4]);
+                        ef[k] = un_idx(w[5]);
+                    }
                 }
             }
             if (capped) {
                 C = NONE;
             } else if (rule == LP_RULE_MIN_INDEX) {
-                C = wave_min_ll(ef);
+                long long e1 = ef[0];
+#pragma unroll
+                for (int k = 1; k < NRE; ++k) e1 = min(e1, ef[k]);
+                C = wave_min_ll(e1);
             } else {
-                const double g = wmin(el);
+                double e1 = el[0];
+#pragma unroll
+                for (int k = 1; k < NRE; ++k) e1 = vmin(e1, el[k]);
+                const double g = wmin(e1);
                 if (g < -tol.cost) {
                     const double ethr = tie_band(g, tol.cost_tie);
-                    double l1[1] = {el}, q1[1] = {eq};
-                    long long i1[1] = {ei};
-                    C = combine_loaded<1>(l1, i1, q1, G, ethr);
+                    C = combine_loaded<NRE>(el, ei, eq, G, ethr);
                     if (C < 0) {                // rare: rescan that block's slice of row 0
                         const long long k0 = 1 + (-1 - C) * cpb, k1 = min(k0 + cpb, A.n + 1);
                         long long best = NONE;
@@ -918,7 +949,9 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         // summary (read from pivot t + 1 on); this pivot's multipliers are
         // stored after it and drained with the next one
         drain_stores();
-        if (!(A.fault == t + 1 && b == min(1u, G - 1) && shard == 0)) {   // fault injection (tests): block 1 (0) never publishes
+        // (W2: only the row blocks publish; fault injection (tests): block 1
+        // (0) never publishes)
+        if (b < GR && !(A.fault == t + 1 && b == min(1u, G - 1) && shard == 0)) {
             unsigned wv = idx32(ib);
             wv = wl(wv, lo32(lb), 0);
             wv = wl(wv, hi32(lb), 1);
@@ -936,7 +969,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         //      travel) the multiplier into its register and to memory
         unsigned w[SEL_NGR];
         SelPoll<SEL_NGR> pr;
-        pr.issue(grR + (b % SEL_NREP_R) * SEL_RSTRIDE, G);
+        pr.issue(grR + (b % SEL_NREP_R) * SEL_RSTRIDE, GR);
         apend = a;
         if (b == 0 && lane == 0) {            // read after the launch only (after the publication:
             *gp(&ctlv->c) = C - 1;            // stores pending at a drain delay the summary)
@@ -1012,7 +1045,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             prow_issue(Rl);
             prow_finish(avv);
         };
-        const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
+        const double rl = (unsigned)lane < GR ? mk_d(w[0], w[1]) : INFINITY;
         const double g = wmin(rl);
         SEL_DONE(g);
         SEL_CLK(20);
@@ -1377,14 +1410,26 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         SEL_CLK(21);
         const bool more = t + 1 < count;
         const unsigned etag = gtag(seq, t, 1);
-        if (more) sel_put_rep<FAST, SEL_NREP_E>(grE, SEL_ESTRIDE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
+        if constexpr (W2) {
+            if (more) sel_put<FAST, SLOTE>(grE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
+        } else {
+            if (more) sel_put_rep<FAST, SEL_NREP_E>(grE, SEL_ESTRIDE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
+        }
         SEL_EV(4);
         SEL_CLK(11);
         // ---- while the summaries travel: the pivot-row values into LDS,
         //      column 0 of the own rows (this pivot's multiplier is a), the
         //      pivot row's register state, the stall bookkeeping, records
-        SelPoll<SEL_NGE> pe;
-        if (more) pe.issue(grE + (b % SEL_NREP_E) * SEL_ESTRIDE, G);
+        SelPoll<SEL_NGE, SLOTE> pe;
+        SelPoll<SEL_NGE, SLOTE> pe2;             // W2: blocks 64 + lane
+        if constexpr (W2) {
+            if (more) {
+                pe.issue(grE, 64);
+                pe2.issue(grE + 64, G - 64);
+            }
+        } else {
+            if (more) pe.issue(grE + (b % SEL_NREP_E) * SEL_ESTRIDE, G);
+        }
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             if (cok[k]) lP[kc[k] * CS + t] = pv[k];
@@ -1438,25 +1483,35 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         }
         // ---- the next pivot's entering column
         SEL_CLK(12);
-        unsigned we[SEL_NGE];
+        unsigned we[SEL_NGE], we2[SEL_NGE];
         if (!pe.finish(etag, we, &ctlv->bar_timeout, spin)) {
             status = LP_DEVICE_ERROR;
             break;
+        }
+        if constexpr (W2) {
+            if (!pe2.finish(etag, we2, &ctlv->bar_timeout, spin)) {
+                status = LP_DEVICE_ERROR;
+                break;
+            }
         }
         SEL_CLK(13);
         SEL_EV(5);
         {
             // the standard rule's minimum first, unconditionally: the loop's
             // bookkeeping below fills its dependency gaps (behind the rule and
-            // stop branches it ran after them)
-            const bool in = (unsigned)lane < G;
+            // stop branches it ran after them).  (W2: lane l holds blocks l
+            // and 64 + l; block order is the columns' order)
+            const bool in = (unsigned)lane < (W2 ? 64u : G);
             const double el2 = in ? mk_d(we[0], we[1]) : INFINITY;
-            const double g2 = wmin(el2);
+            double el2b = INFINITY;
+            if constexpr (W2) el2b = (unsigned)lane + 64 < G ? mk_d(we2[0], we2[1]) : INFINITY;
+            const double g2 = wmin(W2 ? vmin(el2, el2b) : el2);
             SEL_DONE(g2);
             SEL_CLK(18);
             rule = __builtin_amdgcn_readfirstlane(rule);
             stop = __builtin_amdgcn_readfirstlane(stop);
-            const long long ef2 = in ? un_idx(we[5]) : NONE;
+            long long ef2 = in ? un_idx(we[5]) : NONE;
+            if constexpr (W2) ef2 = min(ef2, (unsigned)lane + 64 < G ? un_idx(we2[5]) : NONE);
             const bool capped = cap >= 0 && npiv >= cap;
             long long Cn = NONE;
             int owner = -1;                   // the block that answers (rescan / min-index)
@@ -1469,11 +1524,27 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             } else {
                 if (g2 < -tol.cost) {
                     ethr = tie_band(g2, tol.cost_tie);
-                    const int bs = __builtin_ctzll(bal(el2 <= ethr));   // (lanes >= G: inf)
-                    // (every readlane at once, then the check)
-                    const double qs = rl_d(we[2], we[3], bs);
-                    const long long cb = un_idx(rl32(we[4], bs));
-                    const double pb = rl_d(we[6], we[7], bs);
+                    int bs;
+                    double qs, pb;
+                    long long cb;
+                    if constexpr (W2) {
+                        const u64 ma = bal(el2 <= ethr), mb = bal(el2b <= ethr);
+                        const int fa = ma ? __builtin_ctzll(ma) : 0, fb = mb ? __builtin_ctzll(mb) : 0;
+                        const double qa = rl_d(we[2], we[3], fa), qb2 = rl_d(we2[2], we2[3], fb);
+                        const long long ca = un_idx(rl32(we[4], fa)), cb2 = un_idx(rl32(we2[4], fb));
+                        const double pa = rl_d(we[6], we[7], fa), pb2 = rl_d(we2[6], we2[7], fb);
+                        const bool lo = ma != 0;
+                        bs = lo ? fa : 64 + fb;
+                        qs = lo ? qa : qb2;
+                        cb = lo ? ca : cb2;
+                        pb = lo ? pa : pb2;
+                    } else {
+                        bs = __builtin_ctzll(bal(el2 <= ethr));   // (lanes >= G: inf)
+                        // (every readlane at once, then the check)
+                        qs = rl_d(we[2], we[3], bs);
+                        cb = un_idx(rl32(we[4], bs));
+                        pb = rl_d(we[6], we[7], bs);
+                    }
                     if (qs <= ethr) {
                         Cn = cb;
                         f0 = qs;
@@ -1580,7 +1651,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
 
 }  // namespace
 
-template <int IPL, int NB, bool XR, bool XS>
+template <int IPL, int NB, bool XR, bool XS, bool W2 = false>
 __global__ void __launch_bounds__(GROUP_THREADS)
 k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int first, int fmode, int frule,
       long long fcap)
@@ -1637,11 +1708,19 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
         drain_stores();
         if (lane == 0) st_sc1(&grX[b], ((u64)gtag(seq, 0, 7) << 32) | me);
         unsigned wx[1];
-        if (!sel_gather<1>(grX, G, gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
+        if (!sel_gather<1>(grX, min(G, 64u), gtag(seq, 0, 7), wx, &ctl->bar_timeout, A.spin_max)) {
             if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
             return;
         }
-        const bool same = !((unsigned)lane < G) || wx[0] == me;
+        bool same = !((unsigned)lane < G) || wx[0] == me;
+        if (G > 64) {                          // W2: blocks 64 + lane too
+            unsigned wy[1];
+            if (!sel_gather<1>(grX + 64, G - 64, gtag(seq, 0, 7), wy, &ctl->bar_timeout, A.spin_max)) {
+                if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
+                return;
+            }
+            same = same && (!((unsigned)lane + 64 < G) || wy[0] == me);
+        }
         if (!wall(same)) {
             if (b == 0 && lane == 0) {
                 *gp(&ctl->sel_flags) = 8u | 4u;
@@ -1652,15 +1731,17 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     }
     // diagnostics: 1 one XCD, 4 k_sel, 16 XCD shards
     if (b == 0 && lane == 0 && shard == 0) *gp(&ctl->sel_flags) = XS ? (16u | 4u) : (1u | 4u);
-    sel_body<IPL, NB, XR, true, XS>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
+    sel_body<IPL, NB, XR, true, XS, W2>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
                                     rule, shard);
 }
 
 // ---- geometry and launch ----------------------------------------------------
 namespace {
 
-const void *sel_kernel(int ipl, int nb, bool xr, bool xs)
+const void *sel_kernel(int ipl, int nb, bool xr, bool xs, bool w2 = false)
 {
+    if (w2) return (ipl == 1 && nb == 64 && !xr && !xs) ? reinterpret_cast<const void *>(&k_sel<1, 64, false, false, true>)
+                                                        : nullptr;
 #define SEL_K(I, N) (xr ? reinterpret_cast<const void *>(&k_sel<I, N, true, false>) \
                         : reinterpret_cast<const void *>(&k_sel<I, N, false, false>))
 #define SEL_XS(I) reinterpret_cast<const void *>(&k_sel<I, 64, false, true>)
@@ -1744,6 +1825,32 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
         }
     }
     if (g == 0) return G;
+    // W2 (one XCD, single device, 64 pivots): twice the blocks at one column
+    // per lane -- half the row chain, division and row-0 summary per pivot --
+    // with the first half of the blocks owning the rows as before
+    // (LPGPU_SEL_W2: 1 on, 0 off)
+    static int w2_env = -1;
+    if (w2_env < 0) {
+        const char *v = std::getenv("LPGPU_SEL_W2");
+        w2_env = v ? std::atoi(v) : SEL_W2_DEFAULT;
+    }
+    if (w2_env == 1 && !xs && !xr && share <= 1 && nb == 64 && g == 64 && (n + 127) / 128 <= 64) {
+        const long long cpb2 = (n + 127) / 128;
+        const size_t lds2 = ((size_t)cpb2 * (nb + 2) + 8) * sizeof(double);
+        const int pc2 = sel_per_cu(sel_kernel(1, 64, false, false, true), lds2);
+        if (pc2 >= 1 && 128 <= (long long)pc2 * xcd_cus) {
+            G.g = 128;
+            G.nr = 2;
+            G.ipl = 1;
+            G.rpl = 1;
+            G.xmode = 1;
+            G.sel = nb;
+            G.xs = 0;
+            G.lds = lds2;
+            G.per_cu = pc2;
+            return G;
+        }
+    }
     G.g = g;
     G.nr = 1;
     G.ipl = ipl;
@@ -1763,8 +1870,10 @@ hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int gr
     if (geo.g == 0 || geo.sel == 0 || count < 1 || count > geo.sel) return hipErrorInvalidValue;
     if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
     if (geo.xs && geo.xs != XS_SHARDS) return hipErrorInvalidValue;
-    if (A.rc > 64 * geo.g * (geo.xs ? XS_SHARDS : 1) || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
-    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0, geo.xs > 0);
+    const long long rowblocks = geo.nr == 2 ? geo.g / 2 : geo.g;
+    if (A.rc > 64 * rowblocks * (geo.xs ? XS_SHARDS : 1) || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
+    if (geo.nr == 2 && (geo.g != 128 || xr || geo.xs)) return hipErrorInvalidValue;
+    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0, geo.xs > 0, geo.nr == 2);
     if (!fn) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(geo.g * 8));
     Args a0 = A;

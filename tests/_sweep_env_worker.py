@@ -23,19 +23,35 @@ SHAPES = [("tall", 777, 64, 20, 8), ("mixed", 333, 100, 24, 16), ("tall", 4099, 
 
 def main():
     shapes = SHAPES
-    if os.environ.get("SWEEP_SHAPES"):           # "kind,m,ns,pivots,block;..."
-        shapes = [(f[0], int(f[1]), int(f[2]), int(f[3]), int(f[4]))
+    if os.environ.get("SWEEP_SHAPES"):           # "kind,m,ns,pivots,block[,rule];..."
+        shapes = [(f[0], int(f[1]), int(f[2]), int(f[3]), int(f[4])) + ((int(f[5]),) if len(f) > 5 else ())
                   for f in (x.split(",") for x in os.environ["SWEEP_SHAPES"].split(";"))]
-    for kind, m, ns, k, block in shapes:
+    expect_nr = int(os.environ.get("EXPECT_NR", "0"))   # the persistent selection's summaries per lane
+    for shape in shapes:
+        kind, m, ns, k, block = shape[:5]
+        rule = shape[5] if len(shape) > 5 else 0
         T = gen.tableau(kind, m, ns, 11)
         o = F64Tableau(T.copy())
-        _, olog = o.run(0, k)
+        _, olog = o.run(rule, k)
         e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
         e.upload(T)
         e.set_block(block)
-        st, done = e.run(_lib.RULE_STANDARD, k)
+        st, done = e.run(_lib.RULE_MIN_INDEX if rule else _lib.RULE_STANDARD, k)
         ok = done == len(olog) and e.log().tolist() == olog.tolist() and np.array_equal(e.download(), o.T)
-        print(kind, m, ns, "pivots", done, "ok" if ok else "MISMATCH", flush=True)
+        geo = e.geometry()
+        if expect_nr and (geo["nr"] != expect_nr or e.exchange_path()[1] != 0):
+            print(kind, m, ns, "geometry", geo, "path", e.exchange_path(), flush=True)
+            ok = False
+        print(kind, m, ns, "rule", rule, "pivots", done, "ok" if ok else "MISMATCH", flush=True)
+        if ok and os.environ.get("SOLVE_TOO") == "1":
+            # the whole solve (stall counter, min-index switch, stop rules)
+            # from the same tableau, against the oracle's solve
+            e.upload(T)
+            o2 = F64Tableau(T.copy())
+            ost, olog2, _ = o2.solve(cap=20000)
+            est = e.solve(20000)
+            ok = e.log().tolist() == olog2.tolist() and np.array_equal(e.download(), o2.T)
+            print(kind, m, ns, "solve", len(olog2), "pivots", "ok" if ok else "MISMATCH", est, ost, flush=True)
         e.close()
         if not ok:
             sys.exit(1)

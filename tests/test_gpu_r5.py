@@ -28,3 +28,21 @@ def test_sweep_tail_rows_beyond_one_pass(shapes):
     env = dict(os.environ, LPGPU_SWEEP_CUS="8", SWEEP_SHAPES=shapes)
     run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=280)
     assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
+
+
+@pytest.mark.parametrize("shapes,solve", [
+    ("mixed,4096,4096,136,64", "0"),             # cfg3 at full size: two groups and a padded one
+    ("mixed,4040,2000,150,64;tall,4096,512,100,64", "0"),
+    ("mixed,4040,2000,130,64,1", "0"),           # the min-index rule
+    ("pos,4050,1000,70,64", "1"),                # a whole solve after the run
+])
+def test_sel_w2_bit_exact(shapes, solve):
+    """k_sel's W2 form (LPGPU_SEL_W2=1: 128 blocks of one column per lane,
+    the first 64 owning the rows; two row-0 summaries per lane): the pivot
+    sequence and every bit of the tableau as oracle/lp_f64.c's, the geometry
+    engaged (2 summaries per lane) and no fallback (simplex.py:218-284,
+    tableau.py:295-308)"""
+    worker = os.path.join(os.path.dirname(__file__), "_sweep_env_worker.py")
+    env = dict(os.environ, LPGPU_SEL_W2="1", SWEEP_SHAPES=shapes, EXPECT_NR="2", SOLVE_TOO=solve)
+    run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=280)
+    assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
