@@ -250,7 +250,8 @@ constexpr int SEL_SLOT = 64;
 #define SEL_PIPE 0             // exchanges keep two polls in flight
 #endif
 #ifndef SEL_W2_DEFAULT
-#define SEL_W2_DEFAULT 0       // the 128-block one-column-per-lane form by default (sel_geom)
+#define SEL_W2_DEFAULT 0       // the 128-block one-column-per-lane form by default (sel_geom): off,
+                               // 4.89 against 4.33 us per pivot at cfg3 (round 5 A/B)
 #endif
 #ifndef SEL_POLL1
 #define SEL_POLL1 0            // exchanges poll one word of each summary until it arrives
@@ -1794,19 +1795,30 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
     // the fewest blocks (g) with every lane at most 4 columns, or more where
     // a block's LDS (the pivot values of its columns) leaves too few blocks
     // per CU for g on one XCD
-    const long long g0 = std::max((rps + 63) / 64, (n + 255) / 256);
+    // (LPGPU_SEL_GMIN, A/B: at least that many blocks -- fewer columns per
+    // lane, a shorter row chain -- where they fit)
+    static long long gmin_env = -1;
+    if (gmin_env < 0) {
+        const char *v = std::getenv("LPGPU_SEL_GMIN");
+        gmin_env = v ? std::atoll(v) : 0;
+    }
+    const long long g0 = std::max({(rps + 63) / 64, (n + 255) / 256, std::min(gmin_env, 64LL)});
     const int nb = bmax <= 32 ? 32 : 64;
     long long g = 0, cpb = 0;
     int ipl = 0, per_cu = 0;
     size_t lds = 0;
-    for (long long gc = g0; gc <= 64; gc = gc < 64 && gc + 8 > 64 ? 64 : gc + 8) {
+    bool bad = false;
+    auto fits = [&](long long gc) {
         cpb = (n + gc - 1) / gc;
         ipl = (int)((cpb + 63) / 64);
         if (ipl == 3) ipl = 4;
-        if (ipl > 4) continue;
+        if (ipl > 4) return false;
         lds = ((size_t)cpb * (nb + 2) + 8) * sizeof(double);   // + the row chain's read-ahead slack
         const void *fn = sel_kernel(ipl, nb, xr, xs > 0);
-        if (!fn) return G;
+        if (!fn) {
+            bad = true;
+            return false;
+        }
         per_cu = sel_per_cu(fn, lds);
         if (std::getenv("LPGPU_GEOM_DEBUG"))
             fprintf(stderr, "sel_geom rc %lld n %lld bmax %d xs %d g %lld ipl %d lds %zu per_cu %d xcd_cus %d\n", rc,
@@ -1819,11 +1831,21 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
         // to pass through in dispatch order: with the XCD full, the other
         // rank's launch stalls there and never reaches its own XCD
         const long long need = xs ? gc * std::max(share, 1) : share > 1 ? gc + 1 : gc;
-        if (per_cu >= 1 && need <= (long long)per_cu * xcd_cus) {
-            g = gc;
-            break;
-        }
+        return per_cu >= 1 && need <= (long long)per_cu * xcd_cus;
+    };
+    // XCD shards: 64 blocks first where they fit -- the shard's rows are few
+    // (2/4-GPU ranks of cfg4: 1024 / 2048 per XCD), the columns are what a
+    // lane's chain walks, and two columns per lane beat four: 8192 x 8192
+    // 102.9k -> 109.4k, 16384 x 8192 77.7k -> 80.9k pivots/s (round 5,
+    // scripts/geo_probe.py xs; LPGPU_SEL_XS64=0 for the fewest blocks)
+    static int xs64 = -1;
+    if (xs64 < 0) {
+        const char *v = std::getenv("LPGPU_SEL_XS64");
+        xs64 = v ? std::atoi(v) : 1;
     }
+    if (xs && xs64 && g0 < 64 && fits(64)) g = 64;
+    for (long long gc = g0; g == 0 && !bad && gc <= 64; gc = gc < 64 && gc + 8 > 64 ? 64 : gc + 8)
+        if (fits(gc)) g = gc;
     if (g == 0) return G;
     // W2 (one XCD, single device, 64 pivots): twice the blocks at one column
     // per lane -- half the row chain, division and row-0 summary per pivot --

@@ -39,4 +39,8 @@ print(f"{len(eng) - 1} kernels over {span:.1f} us, busy {busy:.1f} us, idle {spa
       f"({(span - busy) / span:.1%})")
 for name, s in stat.items():
     print(f"  {name[:60]:60s} n {len(s['dur']):3d}  duration {statistics.mean(s['dur']):8.2f} us  "
-          f"gap before {statistics.mean(s['gap']):6.2f} us (min {min(s['gap']):.2f}, max {max(s['gap']):.2f})")
+          f"gap before {statistics.mean(s['gap']):6.2f} us (median {statistics.median(s['gap']):.2f}, "
+          f"min {min(s['gap']):.2f}, max {max(s['gap']):.2f})")
+# idle between kernels of one run (gaps over 100 us are the host between runs)
+inner = [(c[0] - p[1]) / 1e3 for p, c in zip(eng, eng[1:]) if (c[0] - p[1]) / 1e3 < 100]
+print(f"gaps under 100 us: {len(inner)}, total {sum(inner):.1f} us, mean {statistics.mean(inner):.2f} us")

@@ -83,10 +83,11 @@ def test_eight_gpu_rank_geometry_k_sel_xr():
 @pytest.mark.timeout(900)
 def test_two_gpu_rank_geometry_k_sel_xr_xs():
     """one rank of cfg4 on 2 GPUs: 16384 rows as 8 XCD shards (k_sel<XR, XS>),
-    4,096 columns so that both ranks' shards fit every XCD together (G = 32,
-    two columns per lane), automatic 64 pivots per sweep, 136 pivots bit-exact"""
+    4,096 columns so that both ranks' shards fit every XCD together (G = 64,
+    one column per lane: XCD shards take 64 blocks where they fit since
+    round 5), automatic 64 pivots per sweep, 136 pivots bit-exact"""
     outs = _two_ranks(["tall", "32768", "4096", "136", "0", "1e-12", "peer"],
-                      {"LPGPU_XR_XCD": "1", "EXPECT_KERNEL": "k_sel", "EXPECT_XS": "1", "EXPECT_GEOM": "32,2",
+                      {"LPGPU_XR_XCD": "1", "EXPECT_KERNEL": "k_sel", "EXPECT_XS": "1", "EXPECT_GEOM": "64,1",
                        "EXPECT_BLOCK": "64"})
     for out in outs:
         assert "136 pivots" in out, out[-2000:]
