@@ -2207,6 +2207,12 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_LA
 #define SWEEP_LA 0
 #endif
+#ifndef SWEEP_UBASE
+#define SWEEP_UBASE 1          // k_sweep_rl, 4 waves: whole batches' row loads from a wave-uniform base
+#endif                         // (1: buffer loads, 2: global loads, 0: per-lane clamped addresses)
+#ifndef SWEEP_UBASE_W8
+#define SWEEP_UBASE_W8 0       // the same for 8 waves
+#endif
 template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
@@ -2297,16 +2303,44 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     // rows: row 2 q + (l >> 5) of the wave's 8, columns 2 (l & 31) .. +1 of
     // its 64, for q = 0..3 (4 instructions); multipliers: quad (wave >> 1) of
     // the batch, bytes 1 KB x (wave & 1) + 16 l of it (one instruction)
+    // (a whole batch: the batch's first row as a wave-uniform base and each
+    // lane's byte offset from it, fixed for the pass -- the per-lane 64-bit
+    // row x pitch products of the clamped form were ~30 VALU instructions per
+    // batch, a dozen of them quarter-rate multiplies, beside 512 FMAs)
+    unsigned loff[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        loff[q] = (unsigned)(((2 * q + (lane >> 5)) * ld + min(colw + 2 * (lane & 31), ld - 2)) * 8);
     auto issue = [&](long long i, int slot) {
         const long long rb = r0 + i * RW;
         const long long last = r1 - 1;
+        constexpr int UB = W <= 4 ? SWEEP_UBASE : SWEEP_UBASE_W8;
+        if (UB == 1 && rb + RW - 1 <= last) {
+            // buffer loads into LDS: the batch's row as the resource base
+            // (scalar), the lane's offset a 32-bit VGPR
+            const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<double *>(T + rb * ld), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const long long row = min(rb + 2 * q + (lane >> 5), last);
-            const long long cc = min(colw + 2 * (lane & 31), ld - 2);
-            __builtin_amdgcn_global_load_lds(T + row * ld + cc,
-                                             (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
-                                             16, 0, SWEEP_LA);
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rt, (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64], 16,
+                    (int)loff[q], 0, 0, SWEEP_LA);
+        } else if (UB == 2 && rb + RW - 1 <= last) {
+            const char *tb = reinterpret_cast<const char *>(T + rb * ld);   // wave-uniform
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const double *>(tb + loff[q]),
+                                                 (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
+                                                 16, 0, SWEEP_LA);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const long long row = min(rb + 2 * q + (lane >> 5), last);
+                const long long cc = min(colw + 2 * (lane & 31), ld - 2);
+                __builtin_amdgcn_global_load_lds(T + row * ld + cc,
+                                                 (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
+                                                 16, 0, SWEEP_LA);
+            }
         }
         // (W >= 4: quads 0, 1 x halves 0, 1 by waves 0..3; more waves re-copy)
         const int w4 = wave & 3;
