@@ -77,7 +77,7 @@ for step in "$@"; do
             run abenv 900 bash scripts/ab_env.sh "${AB_WL:-cfg3}" "${AB_REPS:-3}" "${S[@]}" ;;
         prof)
             export TMPDIR=/tmp
-            run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py --steps 20 --warmup 5 \
+            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 20 --warmup 5 \
                 --no-cpu-baseline ;;
         pmc)
             # HBM traffic of the sweep per workload: FETCH_SIZE and WRITE_SIZE

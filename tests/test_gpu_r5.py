@@ -48,3 +48,34 @@ def test_sel_w2_bit_exact(shapes, solve):
     env = dict(os.environ, LPGPU_SEL_W2="1", SWEEP_SHAPES=shapes, EXPECT_NR="2", SOLVE_TOO=solve)
     run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=280)
     assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
+
+
+@pytest.mark.parametrize("kind,m,ns,k,blocks,ipl", [
+    ("tall", 8192, 8192, 136, 64, 2),     # a 4-GPU rank of cfg4: 1024 rows per XCD shard, 2 columns per lane
+    ("tall", 9000, 6000, 100, 64, 2),     # 1125-row shards, 18 rows per block (the last 9)
+    ("tall", 12000, 3000, 80, 64, 1),     # 1500-row shards, one column per lane
+])
+def test_xcd_shards_at_64_blocks_bit_exact(kind, m, ns, k, blocks, ipl):
+    """k_sel's XCD shards take 64 blocks where they fit (round 5, sel_geom):
+    shards of 1024-1500 rows, 2 or 1 columns per lane instead of 4 -- the
+    pivot sequence and every bit of the tableau as oracle/lp_f64.c's, no
+    fallback (simplex.py:251-284, tableau.py:295-308)"""
+    import numpy as np
+
+    from lpsol_amd import _lib, generators as gen
+    from oracle.f64 import F64Tableau
+
+    T = gen.tableau(kind, m, ns, 5)
+    e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+    e.upload(T)
+    e.set_block(64)
+    st, done = e.run(_lib.RULE_STANDARD, k)
+    geo = e.geometry()
+    assert geo["kernel"] == "k_sel" and geo["xcd_shards"] == 8, geo
+    assert (geo["blocks"], geo["ipl"]) == (blocks, ipl), geo
+    assert e.exchange_path()[1] == 0
+    o = F64Tableau(T.copy())
+    ost, olog = o.run(0, k)
+    assert done == len(olog) and e.log().tolist() == olog.tolist()
+    assert np.array_equal(e.download().view(np.uint64), o.T.view(np.uint64))
+    e.close()
