@@ -1968,6 +1968,21 @@ __device__ __forceinline__ void rg_pair(double (&x)[8], double m, double pa, dou
                 RGF(6, 10, 14) RGF(7, 10, 15)
         : RG_OUTS(x) : "v"(m), "v"(pa), "v"(pb));
 }
+// four pairs (pivots 8q .. 8q + 7) in one block: one hazard wait for the
+// four multiplier registers instead of one per pair (SWEEP_RGQ)
+#define RGQ(XK, M, P, L) "v_fmac_f64_dpp %" #XK ", -%" #M ", %" #P " row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n"
+__device__ __forceinline__ void rg_quad(double (&x)[8], double m0, double m1, double m2, double m3,
+                                        const double *p)
+{
+    asm("s_nop 1\n" RGQ(0, 8, 12, 0) RGQ(1, 8, 12, 1) RGQ(2, 8, 12, 2) RGQ(3, 8, 12, 3) RGQ(4, 8, 12, 4) RGQ(5, 8, 12, 5) RGQ(6, 8, 12, 6) RGQ(7, 8, 12, 7) RGQ(0, 8, 13, 8) RGQ(1, 8, 13, 9) RGQ(2, 8, 13, 10) RGQ(3, 8, 13, 11) RGQ(4, 8, 13, 12) RGQ(5, 8, 13, 13) RGQ(6, 8, 13, 14) RGQ(7, 8, 13, 15)
+        RGQ(0, 9, 14, 0) RGQ(1, 9, 14, 1) RGQ(2, 9, 14, 2) RGQ(3, 9, 14, 3) RGQ(4, 9, 14, 4) RGQ(5, 9, 14, 5) RGQ(6, 9, 14, 6) RGQ(7, 9, 14, 7) RGQ(0, 9, 15, 8) RGQ(1, 9, 15, 9) RGQ(2, 9, 15, 10) RGQ(3, 9, 15, 11) RGQ(4, 9, 15, 12) RGQ(5, 9, 15, 13) RGQ(6, 9, 15, 14) RGQ(7, 9, 15, 15)
+        RGQ(0, 10, 16, 0) RGQ(1, 10, 16, 1) RGQ(2, 10, 16, 2) RGQ(3, 10, 16, 3) RGQ(4, 10, 16, 4) RGQ(5, 10, 16, 5) RGQ(6, 10, 16, 6) RGQ(7, 10, 16, 7) RGQ(0, 10, 17, 8) RGQ(1, 10, 17, 9) RGQ(2, 10, 17, 10) RGQ(3, 10, 17, 11) RGQ(4, 10, 17, 12) RGQ(5, 10, 17, 13) RGQ(6, 10, 17, 14) RGQ(7, 10, 17, 15)
+        RGQ(0, 11, 18, 0) RGQ(1, 11, 18, 1) RGQ(2, 11, 18, 2) RGQ(3, 11, 18, 3) RGQ(4, 11, 18, 4) RGQ(5, 11, 18, 5) RGQ(6, 11, 18, 6) RGQ(7, 11, 18, 7) RGQ(0, 11, 19, 8) RGQ(1, 11, 19, 9) RGQ(2, 11, 19, 10) RGQ(3, 11, 19, 11) RGQ(4, 11, 19, 12) RGQ(5, 11, 19, 13) RGQ(6, 11, 19, 14) RGQ(7, 11, 19, 15)
+        : RG_OUTS(x)
+        : "v"(m0), "v"(m1), "v"(m2), "v"(m3), "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]),
+          "v"(p[6]), "v"(p[7]));
+}
+#undef RGQ
 #undef RG_OUTS
 #undef RGF
 
@@ -2210,6 +2225,9 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_UBASE
 #define SWEEP_UBASE 1          // k_sweep_rl, 4 waves: whole batches' row loads from a wave-uniform base
 #endif                         // (1: buffer loads, 2: global loads, 0: per-lane clamped addresses)
+#ifndef SWEEP_RGQ
+#define SWEEP_RGQ 1            // k_sweep_rl, 4 waves: the FMAs in blocks of four pivot pairs (one DPP hazard
+#endif                         // wait each; cfg3 sweep 106.7-107.9 -> 104.1-104.6 us; 8 waves: no gain seen)
 #ifndef SWEEP_UBASE_W8
 #define SWEEP_UBASE_W8 0       // the same for 8 waves
 #endif
@@ -2417,8 +2435,13 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
 #pragma unroll
             for (int c = 0; c < NC; ++c) m[c] = mrow[(2 * c + vh) * 4];
         }
+        if constexpr (SWEEP_RGQ && W <= 4 && NC % 4 == 0) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
+            for (int c = 0; c < NC; c += 4) rg_quad(x, m[c], m[c + 1], m[c + 2], m[c + 3], &p[2 * c]);
+        } else {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) rg_pair(x, m[c], p[2 * c], p[2 * c + 1]);
+        }
         // a pivot row s0 of the group in this batch (about one batch in eight
         // at cfg3): it holds P[s0] after pivot s0 and takes only the later
         // pivots -- recomputed here from P (registers) and its multipliers
