@@ -2228,6 +2228,9 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_RGQ
 #define SWEEP_RGQ 1            // k_sweep_rl, 4 waves: the FMAs in blocks of four pivot pairs (one DPP hazard
 #endif                         // wait each; cfg3 sweep 106.7-107.9 -> 104.1-104.6 us; 8 waves: no gain seen)
+#ifndef SWEEP_RGQ_W8
+#define SWEEP_RGQ_W8 0         // ... and for 8 waves (A/B)
+#endif
 #ifndef SWEEP_UBASE_W8
 #define SWEEP_UBASE_W8 0       // the same for 8 waves
 #endif
@@ -2435,7 +2438,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
 #pragma unroll
             for (int c = 0; c < NC; ++c) m[c] = mrow[(2 * c + vh) * 4];
         }
-        if constexpr (SWEEP_RGQ && W <= 4 && NC % 4 == 0) {
+        if constexpr (SWEEP_RGQ && (W <= 4 || SWEEP_RGQ_W8) && NC % 4 == 0) {
 #pragma unroll
             for (int c = 0; c < NC; c += 4) rg_quad(x, m[c], m[c + 1], m[c + 2], m[c + 3], &p[2 * c]);
         } else {
