@@ -2228,6 +2228,9 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_RGQ
 #define SWEEP_RGQ 1            // k_sweep_rl, 4 waves: the FMAs in blocks of four pivot pairs (one DPP hazard
 #endif                         // wait each; cfg3 sweep 106.7-107.9 -> 104.1-104.6 us; 8 waves: no gain seen)
+#ifndef SWEEP_FIXLD
+#define SWEEP_FIXLD 1          // k_sweep_rl fix-up: its LDS reads batched (one wait per pivot row)
+#endif
 #ifndef SWEEP_RGQ_W8
 #define SWEEP_RGQ_W8 0         // ... and for 8 waves (A/B)
 #endif
@@ -2512,12 +2515,21 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     constexpr int NK = NB / 16;
     for (int f = 0; f < nf; ++f) {
         int meta;
-        asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(meta) : "v"(lds_off(&fmeta[f])) : "memory");
-        meta = __builtin_amdgcn_readfirstlane(meta);
-        const int s0 = meta & 255;
         double mk[NK];
+        if constexpr (SWEEP_FIXLD) {
+            // plain LDS reads (the pass's copies have all landed: vmcnt(0)
+            // above): the row's meta word and its 4 multiplier registers in
+            // one round trip, not five
+            meta = __builtin_amdgcn_readfirstlane(fmeta[f]);
 #pragma unroll
-        for (int k = 0; k < NK; ++k) mk[k] = lds_ld64(lds_off(&fixm[f][16 * k + (lane & 15)]));
+            for (int k = 0; k < NK; ++k) mk[k] = fixm[f][16 * k + (lane & 15)];
+        } else {
+            asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(meta) : "v"(lds_off(&fmeta[f])) : "memory");
+            meta = __builtin_amdgcn_readfirstlane(meta);
+#pragma unroll
+            for (int k = 0; k < NK; ++k) mk[k] = lds_ld64(lds_off(&fixm[f][16 * k + (lane & 15)]));
+        }
+        const int s0 = meta & 255;
         double y = pick_p<0, NB, NB>(p, s0);
         fix_chain_dpp<NB>(y, mk, p, s0);
         if (cok) Tout[(r0 + (meta >> 8)) * ld + col] = y;

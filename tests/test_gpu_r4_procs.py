@@ -20,8 +20,10 @@ handles all-gathered over gloo).
 * 2 GPUs: every rank holds 16384 rows and runs k_sel<XR, XS> (the rank's rows
   as 8 XCD shards).  Two such launches on one GPU need 2 G blocks on every
   XCD: at 8,193 columns (G = 64 at two blocks per CU) they cannot share it, so
-  the test takes 4,096 columns (G = 32 at two blocks per CU: 64 per XCD, both
-  ranks resident) -- sel_geom sizes for the co-located ranks (share x G).
+  the tests take 4,096 columns (G = 64 at one column per lane, 4 blocks per
+  CU) and 4,500 (G = 64 at two columns per lane, the product's k_sel<2, 64,
+  XR, XS>; 37.5 KB of LDS per block: 4 per CU, 128 per XCD for both ranks) --
+  sel_geom sizes for the co-located ranks (share x G).
 
 Each: >= 136 pivots at the automatic pivots per sweep (64: two full groups and
 a partial one), LPGPU_STRICT=1 (a timed-out group fails the call), no fallback,
@@ -88,6 +90,19 @@ def test_two_gpu_rank_geometry_k_sel_xr_xs():
     round 5), automatic 64 pivots per sweep, 136 pivots bit-exact"""
     outs = _two_ranks(["tall", "32768", "4096", "136", "0", "1e-12", "peer"],
                       {"LPGPU_XR_XCD": "1", "EXPECT_KERNEL": "k_sel", "EXPECT_XS": "1", "EXPECT_GEOM": "64,1",
+                       "EXPECT_BLOCK": "64"})
+    for out in outs:
+        assert "136 pivots" in out, out[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_two_gpu_rank_geometry_k_sel_xr_xs_two_columns_per_lane():
+    """the 2-GPU rank's product instantiation k_sel<2, 64, XR, XS> (round 5:
+    XCD shards take 64 blocks, two columns per lane at 8,193 columns): 16384
+    rows per rank over 4,500 columns, 136 pivots bit-exact, no fallback"""
+    outs = _two_ranks(["tall", "32768", "4500", "136", "0", "1e-12", "peer"],
+                      {"LPGPU_XR_XCD": "1", "EXPECT_KERNEL": "k_sel", "EXPECT_XS": "1", "EXPECT_GEOM": "64,2",
                        "EXPECT_BLOCK": "64"})
     for out in outs:
         assert "136 pivots" in out, out[-2000:]
