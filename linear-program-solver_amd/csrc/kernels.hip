@@ -2231,6 +2231,9 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_FIXLD
 #define SWEEP_FIXLD 1          // k_sweep_rl fix-up: its LDS reads batched (one wait per pivot row)
 #endif
+#ifndef SWEEP_TAILQ
+#define SWEEP_TAILQ 1          // k_sweep_rl tail rows: the pivot-row check only where the tail holds a pivot row
+#endif
 #ifndef SWEEP_RGQ_W8
 #define SWEEP_RGQ_W8 0         // ... and for 8 waves (A/B)
 #endif
@@ -2561,13 +2564,21 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             double m[NB];
 #pragma unroll
             for (int s = 0; s < NB; ++s) m[s] = M[mq(rr, s)];
+            // (no pivot row of the group among the tail's rows -- nearly
+            // always -- the chain without the per-pivot row check)
+            const bool tpiv = !SWEEP_TAILQ || __ballot(mysr >= t0 && mysr < t1) != 0;
             for (long long c = tcol; c < tend; ++c) {
                 double x = T[rr * ld + c];
                 const double pv = lane < NB ? P[(long long)lane * ld + c] : 0.0;
+                if (tpiv) {
 #pragma unroll
-                for (int s = 0; s < NB; ++s) {
-                    const double ps = readlane_f64(pv, s);
-                    x = rri == __builtin_amdgcn_readlane((int)(unsigned)mysr, s) ? ps : fma(-m[s], ps, x);
+                    for (int s = 0; s < NB; ++s) {
+                        const double ps = readlane_f64(pv, s);
+                        x = rri == __builtin_amdgcn_readlane((int)(unsigned)mysr, s) ? ps : fma(-m[s], ps, x);
+                    }
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NB; ++s) x = fma(-m[s], readlane_f64(pv, s), x);
                 }
                 if (rok) Tout[rr * ld + c] = x;
             }
