@@ -2222,6 +2222,12 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_LA
 #define SWEEP_LA 0
 #endif
+#ifndef SWEEP_LA_T
+#define SWEEP_LA_T SWEEP_LA    // (A/B) the tableau rows' load policy alone
+#endif
+#ifndef SWEEP_LA_OOP
+#define SWEEP_LA_OOP 2         // ... out of place (SA & 2: a tableau far beyond the Infinity Cache,
+#endif                         // its stores non-temporal): the row loads non-temporal too
 #ifndef SWEEP_UBASE
 #define SWEEP_UBASE 1          // k_sweep_rl, 4 waves: whole batches' row loads from a wave-uniform base
 #endif                         // (1: buffer loads, 2: global loads, 0: per-lane clamped addresses)
@@ -2256,6 +2262,12 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     constexpr int RW = 8;                        // rows per batch
     constexpr int NC = NB / 2;                   // multiplier registers (2 pivots x 8 rows each)
     constexpr int XS = W * RW * 64;              // doubles of a slot's rows (W waves x 8 rows x 64 columns)
+    // the tableau rows' load policy: out of place (cfg4: 2.2 GB, far beyond
+    // the Infinity Cache) non-temporal like the stores -- sweep 789-806 ->
+    // 773-785 us, the next selection 6.53-6.55 -> 6.48-6.50 us per pivot;
+    // in place (cfg3) the default, which keeps the tableau in the cache for
+    // the selection (non-temporal there: 102.4-102.6 -> 104.9-106.7 us)
+    constexpr int LAT = (SA & 2) ? SWEEP_LA_OOP : SWEEP_LA_T;
     // a slot's multipliers: two MQ quads, the second QP doubles further on.
     // The multiplier registers of 16 lanes read rows 0-3 of quad 0 and rows
     // 4-7 of quad 1 at the same offsets: 2 KB apart they share LDS banks (a
@@ -2351,14 +2363,14 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             for (int q = 0; q < 4; ++q)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rt, (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64], 16,
-                    (int)loff[q], 0, 0, SWEEP_LA);
+                    (int)loff[q], 0, 0, LAT);
         } else if (UB == 2 && rb + RW - 1 <= last) {
             const char *tb = reinterpret_cast<const char *>(T + rb * ld);   // wave-uniform
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 __builtin_amdgcn_global_load_lds(reinterpret_cast<const double *>(tb + loff[q]),
                                                  (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
-                                                 16, 0, SWEEP_LA);
+                                                 16, 0, LAT);
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -2366,7 +2378,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
                 const long long cc = min(colw + 2 * (lane & 31), ld - 2);
                 __builtin_amdgcn_global_load_lds(T + row * ld + cc,
                                                  (__attribute__((address_space(3))) void *)&xs[slot][(wave * RW + 2 * q) * 64],
-                                                 16, 0, SWEEP_LA);
+                                                 16, 0, LAT);
             }
         }
         // (W >= 4: quads 0, 1 x halves 0, 1 by waves 0..3; more waves re-copy)
