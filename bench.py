@@ -371,6 +371,38 @@ def dump_stamps(eng, geo: dict, block: int, rank: int) -> None:
              geometry=np.array([geo.get(k, 0) for k in ("blocks", "ipl", "xcd_shards")]))
 
 
+def profile_every_for(rows: int, n: int, steps: int, requested: int) -> int:
+    """launches timed with HIP events: every one where a sweep is long (a
+    local tableau beyond 1 GB: cfg4 on one GPU, ~800 us per sweep -- an
+    event pair's ~2 us is 0.3 %, and sampling every 4th read a biased subset:
+    VERDICT r5), else every 4th (every 8th from 64 steps; every launch costs
+    cfg3's 0.4 ms groups ~2 %: 156.3k against 159.4k pivots/s)"""
+    if requested > 0:
+        return requested
+    if 8.0 * rows * (n + 1) > 1e9:
+        return 1
+    return 4 if steps < 64 else 8
+
+
+def sweep_clock_summary(eng, steps: int) -> dict:
+    """the shader clock of the timed sweeps (k_sweep_rl's block 0 records
+    cycles and 100 MHz ticks of its pass, Args::sweep_clk): with the event
+    times it tells a clock effect (the same cycles at a lower clock) from a
+    memory one (more cycles at the same clock)"""
+    try:
+        c = eng.sweep_clocks(steps)
+    except Exception as ex:                      # noqa: BLE001 -- a diagnostic only
+        return {"error": str(ex)}
+    c = c[-steps:]
+    if len(c) == 0:
+        return {"launches": 0}
+    ghz = c[:, 1] / (c[:, 2] / 1e8) / 1e9
+    us = c[:, 2] / 100.0
+    return {"launches": int(len(c)), "ghz_mean": float(ghz.mean()), "ghz_min": float(ghz.min()),
+            "ghz_max": float(ghz.max()), "block0_us_mean": float(us.mean()),
+            "kcycles_mean": float(c[:, 1].mean() / 1e3)}
+
+
 def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int, heater=None, heat_ms: float = 0.0):
     """device warm-up on the heater (untimed, another tableau; closed right
     after it), warmup groups, then exactly `steps` timed groups bracketed by the barrier + stream sync
@@ -394,6 +426,7 @@ def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int, hea
     upd_ms, upd_n = eng.update_time()
     sel_ms, sel_n = eng.select_time()
     eng.profile(False)
+    heat["sweep_clock"] = sweep_clock_summary(eng, steps)
     return t1 - t0, upd_ms / max(upd_n, 1), (sel_ms / sel_n if sel_n else 0.0), upd_n, sel_n, heat
 
 
@@ -417,8 +450,10 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
         heater.set_block(block)
     upload(engs, kind, m, ns, spans, heaters=[heater] if heater else None)
     xw0 = engs[0].xwait()
+    every = profile_every_for(spans[0][1] - spans[0][0] + 1, n, steps, every)
     elapsed, sw_ms, sel_ms, sw_n, sel_n, heat = timed_run(engs[0], steps, warmup, block, lambda: None, every,
                                                           heater, heat_ms)
+    clock = heat.pop("sweep_clock", None)
     xw1 = engs[0].xwait()
     path, fallbacks = engs[0].exchange_path()
     geo = engs[0].geometry()
@@ -432,7 +467,7 @@ def single_gpu_leg(name: str, steps: int, warmup: int, block: int, every: int, d
                                        if xw1[1] > xw0[1] else 0.0)
     acc.update(block=block, path=_lib.PATH_NAMES.get(path, path), fallbacks=fallbacks, device_warmup=heat,
                sweep_avg_us=sw_ms * 1e3, sweep_launches_timed=sw_n, selection_launches_timed=sel_n,
-               selection_avg_launch_us=sel_ms * 1e3)
+               selection_avg_launch_us=sel_ms * 1e3, sweep_clock=clock, profile_every=every)
     for e in reversed(engs):
         e.close()
     return acc
@@ -470,11 +505,6 @@ def main():
                     help="instead of the benchmark: cfg1/cfg2/cfg5 on GPU 0 next to the "
                          "exact-Fraction CPU path, one JSON line each")
     args = ap.parse_args()
-    if args.profile_every <= 0:
-        # a short run (the driver's 20 steps) would time only 2-3 launches at
-        # every 8th; every launch costs cfg3 ~2 % of its wall-clock rate
-        # (events around each 0.4 ms group: 156.3k against 159.4k pivots/s)
-        args.profile_every = 4 if args.steps < 64 else 8
     if args.configs:
         config_table()
         return
@@ -550,8 +580,10 @@ def main():
             heater.set_block(B)
         upload([eng], kind, m, ns, [(rb, re_)], heaters=[heater])
         xw0 = eng.xwait()
+        every = profile_every_for(re_ - rb + 1, n, args.steps, args.profile_every)
         elapsed, sw_ms, sel_ms, sw_n, sel_n, heat = timed_run(eng, args.steps, args.warmup, B, dist.barrier,
-                                                              args.profile_every, heater, args.device_warmup_ms)
+                                                              every, heater, args.device_warmup_ms)
+        clock = heat.pop("sweep_clock", None)
         if heater is None and args.device_warmup_ms > 0:
             heat["skipped"] = "ranks share a GPU"
         xw1 = eng.xwait()
@@ -579,7 +611,8 @@ def main():
         sweep_ms = sw_ms
         acc = accounting(args.steps, B, elapsed, sw_ms, sel_ms, local_rows, n)
         acc.update(fallbacks=fallbacks, sweep_launches_timed=sw_n, selection_launches_timed=sel_n, device_warmup=heat,
-                   selection_avg_launch_us=sel_ms * 1e3, selection_kernel=kern,
+                   selection_avg_launch_us=sel_ms * 1e3, selection_kernel=kern, sweep_clock=clock,
+                   profile_every=every,
                    xrank_hop_us_per_pivot=hop_us,
                    ranks=[{"rank": r, "host": h, "device": d, "selection_kernel": k, "path": pth, "fallbacks": fb}
                           for h, d, r, k, pth, fb in ids],
@@ -632,6 +665,11 @@ def main():
             "f64_fma_per_launch": acc["sweep_fma_per_launch"],
             "f64_TFLOPs": acc["sweep_f64_TFLOPs"],
             "f64_peak_TFLOPs": F64_PEAK_TFLOPS,
+            # launches timed with events (every one at cfg4) and the shader
+            # clock over them (block 0's cycles / 100 MHz ticks per launch)
+            "launches_timed": acc["sweep_launches_timed"],
+            "timed_every": acc.get("profile_every"),
+            "shader_clock": acc.get("sweep_clock"),
         },
         "selection": {
             "kernel": f"{acc.get('selection_kernel', 'k_group')} (persistent pivot selection, latency-bound)",
@@ -665,7 +703,9 @@ def main():
                          / HBM_PEAK_GBPS,
                          "traffic": load_traffic(args.traffic_json, c3["block"], "cfg3", digest),
                          "bytes_per_launch": c3["sweep_bytes_per_launch"],
-                         "avg_launch_us": c3["sweep_avg_us"], "time_share": c3["sweep_time_share"]},
+                         "avg_launch_us": c3["sweep_avg_us"], "time_share": c3["sweep_time_share"],
+                         "launches_timed": c3["sweep_launches_timed"], "timed_every": c3["profile_every"],
+                         "shader_clock": c3["sweep_clock"]},
             "selection": {"kernel": c3["selection_kernel"], "us_per_pivot": c3["selection_us_per_pivot"],
                           "time_share": c3["selection_time_share"]},
             "path": c3["path"], "fallbacks": c3["fallbacks"],

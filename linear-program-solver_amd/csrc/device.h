@@ -137,7 +137,17 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 // numerics shared by every kernel
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ double tie_band(double g, double tie) { return g + tie * fabs(g); }
+// g + tie |g|, clamped to the largest double: a band that overflows holds
+// every finite value (as oracle/lp_f64.c's +inf band does for its finite
+// candidates) but never +inf, the "no candidate" marker of every summary, so
+// a ballot of `x <= band` can only name a lane that has a candidate (ADVICE
+// r5: a finite g near DBL_MAX made +inf pass and a speculative row load
+// index NONE)
+__device__ __forceinline__ double tie_band(double g, double tie)
+{
+    const double r = g + tie * fabs(g);
+    return r <= 1.7976931348623157e308 ? r : 1.7976931348623157e308;
+}
 
 // ratio of one constraint row; ok=false if a <= tol.pivot   (simplex.py:273-276)
 __device__ __forceinline__ double row_ratio(double a, double b, const lp_tol &tol, bool &ok)

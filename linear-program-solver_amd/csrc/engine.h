@@ -181,7 +181,14 @@ struct Args {
     double *Tout;
     unsigned *dflips;
     unsigned flipseq;
+    // per-launch clocks of the sweep (k_sweep_rl, block 0): launch lseq writes
+    // entry lseq % SWEEP_CLK_RING = {lseq, shader cycles, 100 MHz ticks, start
+    // tick} of its block 0's pass -- the shader clock during each launch
+    // (lpdiag_sweep_clocks, bench.py, scripts/sweep_clock.py)
+    unsigned long long *sweep_clk;
+    unsigned sweep_lseq;
 };
+constexpr int SWEEP_CLK_RING = 1024;
 
 // exchange buffer layout (granules of 8 bytes), see kernels.hip (XR)
 constexpr int NRANK_MAX = 64;

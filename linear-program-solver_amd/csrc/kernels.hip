@@ -1455,21 +1455,16 @@ k_group(Args A0, const Args *As, int gper, int grp, int count, int from_erec, un
 
 // ---------------------------------------------------------------------------
 // K3: the sweep (tableau.py:305-308 -> :269-289 for a whole group).  T <- T
-//   with the group's deferred pivots 0..ndef-1 applied, in place.
-//   A workgroup of W waves owns a 128-column strip
-//   (2 columns per lane, 16-byte accesses) of a contiguous run of rows; the
-//   strip's slice of P is staged in LDS ONCE for the whole run (not once per
-//   tile as in k_sweep).  Each wave walks batches of RW rows (wave w takes
-//   batches w, w + W, ...) and keeps the NEXT batch's rows and multipliers in
-//   flight while it updates the current one, so the loads of every wave
-//   overlap its FMAs instead of alternating with them (k_sweep's tile goes
-//   load-all / barrier / compute / store).  A
-//   batch's multipliers (wave-uniform) go through a per-wave LDS slot and are
-//   read as 16-byte broadcasts; no workgroup barrier after the P staging.
+//   with the group's deferred pivots 0..ndef-1 applied.  Two kernels:
+//   k_sweep_rl (below) for groups of 49..64 pivots -- the automatic depth of
+//   cfg3 and cfg4, so the bench's kernel -- and k_sweep_dp2 for shorter ones
+//   (a call's short last group, explicit pivots, the per-pivot path's 32).
 //   Pivots nd..NB-1 are padding with P = 0 and multiplier 0: fma(-0, 0, x)
 //   == x for every x.  Every element gets exactly the float64 operations of
 //   an immediate update in pivot order (upd()): bit-identical to
-//   oracle/lp_f64.c for every group size.
+//   oracle/lp_f64.c for every group size.  (Rounds 1-2's k_sweep_st and
+//   k_sweep_dp, LDS- and register-broadcast strips, were removed in round 6:
+//   k_sweep_rl replaced them at 64 pivots)
 // ---------------------------------------------------------------------------
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -1481,160 +1476,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base)
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
 }
 
-// One strip of 128 columns over rows [r0, r1): the strip's slice of P is
-// staged in LDS (sp), each wave walks RW-row batches and keeps the NEXT
-// batch's rows and multipliers in flight while it applies the pivots to the
-// current one.  Shared by the in-place sweep (one strip and row run per
-// workgroup) and the pipelined sweep (tiles taken from a counter).
-template <int W, int RW, int NB, int LA, int SA>
-__device__ __forceinline__ void sweep_strip(double2 (&sp)[NB][64], double2 (&sm)[W][NB][RW / 2],
-                                            const long long (&sr)[NB], const double *T, double *Tout,
-                                            const double *__restrict__ P, const double *__restrict__ M,
-                                            int nd, long long ld, long long rows, int strip,
-                                            long long r0, long long r1)
-{
-    constexpr int MPL = NB * RW / 64;           // multipliers per lane per batch
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // lanes past the last column (ld % 128 == 64) shadow the last lane's
-    // columns: same loads, same results, same bytes stored
-    const long long c0 = (long long)strip * 128;
-    const int lo = min(lane * 2, (int)(ld - c0) - 2);
-    const int lob = lo * 8;                     // lane byte offset within a row
-    const int ldb = (int)(ld * 8);              // row pitch in bytes
-    const double *Ts = T + c0;
-    double *Tos = Tout + c0;
-    for (int s = wave; s < NB; s += W)
-        sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
-    // element e = lane + 64 q of a batch's multipliers: pivot e / RW, row e % RW
-    // (padding pivots read pivot 0's and are zeroed)
-    int mof[MPL];
-    bool mlive[MPL];
-#pragma unroll
-    for (int q = 0; q < MPL; ++q) {
-        const int e = lane + 64 * q, s = e / RW;
-        mof[q] = (s < nd ? s : 0) * 4;           // + min(row in batch, kmax) (4-row quads, mi())
-        mlive[q] = s < nd;
-    }
-    // rows past r1 re-load row r1 - 1 (in bounds) and are never stored
-    auto load = [&](double2 (&x)[RW], double (&mv)[MPL], long long rb) {
-        const int kmax = (int)(r1 - 1 - rb);
-        const __amdgpu_buffer_rsrc_t rt = buf_rsrc(Ts + rb * ld);
-        const __amdgpu_buffer_rsrc_t rm = buf_rsrc(M + (rb >> 2) * (4 * BMAX));
-#pragma unroll
-        for (int q = 0; q < MPL; ++q) {
-            const int k = (lane + 64 * q) % RW;
-            // raw value: the padding select happens when it is staged, so
-            // nothing waits for this load before the next batch
-            mv[q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rm, (mof[q] + min(k, kmax)) * 8, 0, 0));
-        }
-#pragma unroll
-        for (int k = 0; k < RW; ++k)
-            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rt, lob, min(k, kmax) * ldb, LA));
-    };
-    double *smw = reinterpret_cast<double *>(&sm[wave][0][0]);
-    const long long step = (long long)W * RW;
-    long long rb = r0 + (long long)wave * RW;
-    double2 xn[RW];
-    double mn[MPL];
-    if (rb < r1) load(xn, mn, rb);
-    __syncthreads();                            // sp, sr staged
-    for (; rb < r1; rb += step) {
-        double2 x[RW];
-#pragma unroll
-        for (int k = 0; k < RW; ++k) x[k] = xn[k];
-        // the wave's own LDS slot: its previous batch's reads are complete
-        // (LDS operations of one wave execute in order)
-#pragma unroll
-        for (int q = 0; q < MPL; ++q) smw[lane + 64 * q] = mlive[q] ? mn[q] : 0.0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const long long rn = rb + step;
-        if (rn < r1) load(xn, mn, rn);
-        // rows past r1 (k > kmax) compute row r1 - 1 again (same loads, same
-        // multipliers, same pivot-row test) and store the same bytes there,
-        // so every load and store is unconditional (exact wait counts)
-        const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
-        const long long R = sr[lane % NB];
-        if (__builtin_expect(__ballot(R >= rb && R < rb + RW) == 0, 1)) {
-#pragma unroll 2
-            for (int s = 0; s < NB; ++s) {
-                const double2 pv = sp[s][lane];
-                double2 f[RW / 2];
-#pragma unroll
-                for (int h = 0; h < RW / 2; ++h) f[h] = sm[wave][s][h];
-#pragma unroll
-                for (int h = 0; h < RW / 2; ++h) {
-                    x[2 * h].x = fma(-f[h].x, pv.x, x[2 * h].x);
-                    x[2 * h].y = fma(-f[h].x, pv.y, x[2 * h].y);
-                    x[2 * h + 1].x = fma(-f[h].y, pv.x, x[2 * h + 1].x);
-                    x[2 * h + 1].y = fma(-f[h].y, pv.y, x[2 * h + 1].y);
-                }
-            }
-        } else {
-#pragma unroll 1
-            for (int s = 0; s < NB; ++s) {
-                const double2 pv = sp[s][lane];
-                const long long kr = sr[s] - rb;   // padding pivots: -2 - rb, never a row
-                const double *f = reinterpret_cast<const double *>(&sm[wave][s][0]);
-#pragma unroll
-                for (int k = 0; k < RW; ++k) {
-                    const double fk = f[k];
-                    const double2 y = make_double2(fma(-fk, pv.x, x[k].x), fma(-fk, pv.y, x[k].y));
-                    x[k] = min(k, kmax) == kr ? pv : y;
-                }
-            }
-        }
-        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(Tos + rb * ld);
-#pragma unroll
-        for (int k = 0; k < RW; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
-    }
-}
-
-// LA / SA: cache-policy bits of the tableau's loads / stores (0 default, 2 nt,
-// 16 sc1 = write-through)
-template <int W, int RW, int NB, int LA = 0, int SA = 0>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(NB <= 32 ? 6 : 2, 8)))
-k_sweep_st(const double *T, double *Tout, const double *__restrict__ P,
-           const double *__restrict__ M, const long long *__restrict__ dR,
-           const Ctl *__restrict__ ctl, long long ld, long long rows, int grp, int nstrips,
-           long long run)
-{
-    static_assert(RW == 4, "k_sweep_st: batches are the 4-row quads of M (mi())");
-    static_assert(RW % 2 == 0 && NB <= BMAX && (NB * RW) % 64 == 0, "k_sweep_st: batch shape");
-    __shared__ double2 sp[NB][64];              // the strip's slice of P
-    __shared__ double2 sm[W][NB][RW / 2];       // per wave: the current batch's multipliers
-    __shared__ long long sr[NB];
-    const int nd = (int)ctl->ndef[grp];         // <= NB (the host's bound)
-    // a group whose selection timed out is redone from its start by the host
-    if (nd == 0 || ctl->bar_timeout) return;
-    // block b: strip b % nstrips of row run b / nstrips.  Consecutive blocks
-    // are dealt round-robin over the 8 XCDs, so each run's multipliers and
-    // each strip's slice of P are fetched into every XCD's L2 about once
-    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
-    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
-    const long long r1 = min(rows, r0 + run);
-    if (r0 >= r1) return;
-    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
-    sweep_strip<W, RW, NB, LA, SA>(sp, sm, sr, T, Tout, P, M, nd, ld, rows, strip, r0, r1);
-}
-
 // ---------------------------------------------------------------------------
-// K3': the sweep with the multipliers broadcast by DPP (k_sweep_dp).  Same
-//   tiling as k_sweep_st (a workgroup owns a 128-column strip of a run of
-//   rows, 2 columns per lane, 4-row batches per wave, the strip's slice of P
-//   staged in LDS once), but a batch's multipliers never pass through LDS:
-//   every lane loads them straight into registers, 16 values per register --
-//   value v = 4 s' + k (pivot 4 c + s', batch row k) of chunk c sits in lane
-//   v of each 16-lane row -- and the FMA reads the one it needs with a
-//   row_newbcast DPP operand:
-//       v_fmac_f64_dpp x, -m, p row_newbcast:v      (x <- fma(-m[v], p, x))
-//   so per pivot and lane the LDS serves one 16-byte read (P) for 8 FMAs,
-//   a third of k_sweep_st's LDS traffic, and no instruction is spent on the
-//   broadcast.  Same float64 operations in the same order as upd(): bit-
-//   identical to k_sweep_st and oracle/lp_f64.c.
+// The multipliers broadcast by DPP: a 4-pivot chunk's multipliers of a 4-row
+// batch sit in one register, value v = 4 s' + k (pivot 4 c + s', batch row
+// k) in lane v of each 16-lane row, and the FMA reads the one it needs with a
+// row_newbcast DPP operand:
+//     v_fmac_f64_dpp x, -m, p row_newbcast:v      (x <- fma(-m[v], p, x))
+// -- no instruction is spent on the broadcast.
 // ---------------------------------------------------------------------------
 
 // pivots 4c + 2h, 4c + 2h + 1 of one batch (4 rows x 2 columns per lane): 16
@@ -1661,130 +1509,11 @@ __device__ __forceinline__ void dp_half(double2 (&x)[4], double m, double2 p0, d
 #undef DPP_PIVOT
 #undef DPF
 
-template <int W, int NB, int SA, int LA = 0>
-__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4, 8)))
-k_sweep_dp(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
-           const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
-           int nstrips, long long run, long long tail)
-{
-    constexpr int RW = 4;                        // rows per batch (4 x 4 = 16 values a register)
-    constexpr int NM = NB / 4;                   // multiplier registers (4 pivots each)
-    static_assert(NB % 4 == 0 && NB <= BMAX, "k_sweep_dp: pivots per sweep");
-    __shared__ double2 sp[NB][64];               // the strip's slice of P
-    __shared__ long long sr[NB];
-    const int nd = (int)ctl->ndef[grp];          // <= NB (the host's bound)
-    if (nd == 0 || ctl->bar_timeout) return;     // nothing deferred / group redone by the host
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int ldb = (int)(ld * 8);
-    if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
-    // this lane's multiplier slot of register c: pivot 4 c + q / 4, row q % 4
-    // (q = lane % 16); pivots past nd read pivot nd - 1's (finite; their P is 0)
-    const int q = lane & 15, qs = q >> 2, qk = q & 3;
-    const int nch = (nd + 3) >> 2;               // chunks holding live pivots
-    // rows [r0, r1) of one strip
-    auto piece = [&](int strip, long long r0, long long r1) {
-    const long long c0 = (long long)strip * 128;
-    const int lo = min(lane * 2, (int)(ld - c0) - 2);
-    const int lob = lo * 8;
-    const double *Ts = T + c0;
-    double *Tos = Tout + c0;
-    for (int s = wave; s < NB; s += W)
-        sp[s][lane] = s < nd ? *reinterpret_cast<const double2 *>(P + s * ld + c0 + lo) : make_double2(0.0, 0.0);
-    // the multipliers of chunk c of the batch at rb (one register)
-    auto load_m = [&](long long rb, int c) {
-        const int mk = min(qk, (int)(r1 - 1 - rb));
-        const int sv = min(4 * c + qs, nd - 1);
-        return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(buf_rsrc(M + (rb >> 2) * (4 * BMAX)), (sv * 4 + mk) * 8, 0, 0));
-    };
-    auto load_x = [&](double2 (&x)[RW], long long rb) {
-        const int kmax = (int)(r1 - 1 - rb);
-        const __amdgpu_buffer_rsrc_t rt = buf_rsrc(Ts + rb * ld);
-#pragma unroll
-        for (int k = 0; k < RW; ++k)
-            x[k] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rt, lob, min(k, kmax) * ldb, LA));
-    };
-    const long long step = (long long)W * RW;
-    long long rb = r0 + (long long)wave * RW;
-    // the next batch's rows are in flight while the current one is updated
-    // (two batches ahead, 3 waves per SIMD: 5-25 % slower)
-    double2 xn[RW];
-    double m[NM];                                // the current batch's multipliers
-    if (rb < r1) {
-        load_x(xn, rb);
-#pragma unroll
-        for (int c = 0; c < NM; ++c) m[c] = load_m(rb, c);
-    }
-    __syncthreads();                             // sp, sr staged
-    for (; rb < r1; rb += step) {
-        double2 x[RW];
-#pragma unroll
-        for (int k = 0; k < RW; ++k) x[k] = xn[k];
-        const long long rn = rb + step;
-        const bool more = rn < r1;
-        if (more) load_x(xn, rn);
-        const int kmax = (int)min((long long)RW - 1, r1 - 1 - rb);
-        // chunk c's register is reloaded with the next batch's as soon as it
-        // has been used (one set of multiplier registers)
-        // the next pivot pair's P is read from LDS while this pair's FMAs run
-        double2 pa = sp[0][lane], pb = sp[1][lane];
-#pragma unroll
-        for (int c = 0; c < NM; ++c) {
-            if (c < nch) {                       // wave-uniform
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int s2 = 4 * c + 2 * h + 2;
-                    const double2 qa = sp[s2 < NB ? s2 : 0][lane], qb = sp[s2 + 1 < NB ? s2 + 1 : 1][lane];
-                    dp_half(x, m[c], pa, pb, h);
-                    pa = qa;
-                    pb = qb;
-                }
-            }
-            if (more) m[c] = load_m(rn, c);
-        }
-        // a row that was pivot row s of the group holds P[s] after pivot s
-        // and then takes the later pivots only: recomputed from P (rare --
-        // the chunks above gave it a meaningless value)
-        const long long R = sr[lane % NB];
-        if (__builtin_expect(__ballot(R >= rb && R < rb + RW) != 0, 0)) {
-#pragma unroll
-            for (int k = 0; k < RW; ++k) {
-                const long long row = rb + min(k, kmax);
-                int sl = -1;
-                for (int s = 0; s < nd; ++s)
-                    if (sr[s] == row) sl = s;
-                if (sl >= 0) {
-                    double2 y = sp[sl][lane];
-                    for (int s = sl + 1; s < nd; ++s) {
-                        const double f = M[mq(row, s)];
-                        const double2 pv = sp[s][lane];
-                        y = make_double2(fma(-f, pv.x, y.x), fma(-f, pv.y, y.y));
-                    }
-                    x[k] = y;
-                }
-            }
-        }
-        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(Tos + rb * ld);
-#pragma unroll
-        for (int k = 0; k < RW; ++k)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, x[k]), ro, lob, min(k, kmax) * ldb, SA);
-    }
-    };
-    const int strip = (int)(blockIdx.x % (unsigned)nstrips);
-    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
-    piece(strip, r0, min(rows, r0 + run));
-    if (tail > 0) {                              // as in k_sweep_dp2
-        const long long t0 = (long long)blockIdx.x * tail;
-        if (t0 < rows) {
-            __syncthreads();
-            piece(nstrips, t0, min(rows, t0 + tail));
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
-// K3'': k_sweep_dp with the multipliers staged through a per-wave LDS slot
-//   (k_sweep_dp2, LPGPU_SWEEP_DP=2, A/B).  A batch's 4 x NB multipliers
+// K3'': k_sweep_dp2, the sweep of groups of up to 48 pivots: a workgroup of
+//   W waves owns a 128-column strip (2 columns per lane, 16-byte accesses) of
+//   a run of rows, the strip's slice of P staged in LDS once, each wave on
+//   4-row batches with the next batch in flight.  A batch's 4 x NB multipliers
 //   arrive with 2 coalesced 16-byte loads per lane (lane l: pivot l's four
 //   rows, half a batch per 32 lanes) instead of NB/4 replicated 8-byte loads,
 //   are written to the slot half a batch at a time, and each 4-pivot chunk's
@@ -2050,44 +1779,6 @@ __device__ __forceinline__ void lds_mult(double (&m)[NC], unsigned a)
     }
 }
 
-// k_sweep_rl's pivot-row fix-up: the batch row's multipliers of pivots
-// 8 H .. 8 H + 7 (one MQ quad: 32 bytes apart) from LDS, uniform addresses
-template <int H>
-__device__ __forceinline__ void lds_mrow8(double (&v)[8], unsigned a)
-{
-    asm volatile("ds_read_b64 %0, %8 offset:%9\n ds_read_b64 %1, %8 offset:%10\n ds_read_b64 %2, %8 offset:%11\n"
-                 "ds_read_b64 %3, %8 offset:%12\n ds_read_b64 %4, %8 offset:%13\n ds_read_b64 %5, %8 offset:%14\n"
-                 "ds_read_b64 %6, %8 offset:%15\n ds_read_b64 %7, %8 offset:%16\n s_waitcnt lgkmcnt(0)"
-                 : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3]), "=v"(v[4]), "=v"(v[5]), "=v"(v[6]), "=v"(v[7])
-                 : "v"(a), "n"(256 * H), "n"(256 * H + 32), "n"(256 * H + 64), "n"(256 * H + 96), "n"(256 * H + 128),
-                   "n"(256 * H + 160), "n"(256 * H + 192), "n"(256 * H + 224));
-}
-// y (pivot row s0, this lane's column) <- P[s0] with pivots s0 + 1 .. NB - 1
-// applied, their multipliers of that row read from LDS at a (+ 32 s bytes),
-// 8 at a time; chunks that end at or before s0 are skipped.  (A branch-free
-// form -- 32 multipliers per read, the pivots up to s0 masked to exact
-// no-ops -- measured 170 against 122 us per cfg3 launch: its registers cost
-// the main loop)
-template <int NB, int H = 0>
-__device__ __forceinline__ void fix_chain(double &y, const double (&p)[NB], unsigned a, int s0)
-{
-    if constexpr (H == 0) {
-#pragma unroll
-        for (int s = 0; s < NB; ++s)
-            if (s == s0) y = p[s];
-    }
-    if constexpr (H < NB / 8) {
-        if (8 * H + 7 > s0) {
-            double v[8];
-            lds_mrow8<H>(v, a);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (8 * H + j > s0) y = fma(-v[j], p[8 * H + j], y);
-        }
-        fix_chain<NB, H + 1>(y, p, a, s0);
-    }
-}
-
 // pivots 16 K + j0 .. 16 K + j1 - 1 of a pivot-row chain: y <- fma(-m[lane
 // 16 K + j of the 16-lane row], p[16 K + j], y), the multiplier broadcast by
 // DPP (lane l of mk holds pivot 16 K + (l & 15)'s multiplier of the row)
@@ -2234,12 +1925,6 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_RGQ
 #define SWEEP_RGQ 1            // k_sweep_rl, 4 waves: the FMAs in blocks of four pivot pairs (one DPP hazard
 #endif                         // wait each; cfg3 sweep 106.7-107.9 -> 104.1-104.6 us; 8 waves: no gain seen)
-#ifndef SWEEP_FIXLD
-#define SWEEP_FIXLD 1          // k_sweep_rl fix-up: its LDS reads batched (one wait per pivot row)
-#endif
-#ifndef SWEEP_TAILQ
-#define SWEEP_TAILQ 1          // k_sweep_rl tail rows: the pivot-row check only where the tail holds a pivot row
-#endif
 #ifndef SWEEP_RGQ_W8
 #define SWEEP_RGQ_W8 0         // ... and for 8 waves (A/B)
 #endif
@@ -2251,7 +1936,7 @@ __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
            int nstrips, long long run, long long tail, long long tcol, long long tend, int nexp,
-           unsigned *dflips, unsigned flipseq)
+           unsigned *dflips, unsigned flipseq, unsigned long long *clk, unsigned lseq)
 {
     // tail > 0: the grid covers strips [0, nstrips) of the columns and the 64
     // columns from tcol (the tableau's last columns: n + 1 is rarely a
@@ -2298,6 +1983,10 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     // out of place (Tout != T): this sweep ran -- the host's record of which
     // buffer holds the tableau (every block takes the same branch above)
     if (dflips && blockIdx.x == 0 && threadIdx.x == 0) *dflips = flipseq;
+    // block 0's clocks over its pass (Args::sweep_clk): the shader clock of
+    // the launch = cycles / 100 MHz ticks (every block is resident from the
+    // start and the runs finish together, so block 0 spans the launch)
+    const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
     auto srow = [&](int s) -> long long { return sr[s]; };
     const int strip = (int)(blockIdx.x % (unsigned)nstrips);
@@ -2467,20 +2156,6 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         // at cfg3): it holds P[s0] after pivot s0 and takes only the later
         // pivots -- recomputed here from P (registers) and its multipliers
         // (this batch's LDS slot), not re-read from memory after the pass
-#ifdef SWEEP_FIX_INLOOP
-        for (u64 hit = __ballot(mysr >= rb && mysr <= rb + kmax); hit; hit &= hit - 1) {
-            const int s0 = __builtin_ctzll(hit);
-            const int k = (int)(__builtin_amdgcn_readlane((int)(unsigned)mysr, s0) - (int)(unsigned)rb);
-            double y = 0.0;
-            fix_chain<NB>(y, p, lds_off(&ms[slot][(k >> 2) * (4 * BMAX + QP) + (k & 3)]), s0);
-            // (a last, partial batch stores row kmax from every x[k >= kmax]:
-            // all of them take the fixed value)
-#pragma unroll
-            for (int kk = 0; kk < RW; ++kk)
-                if (min(kk, kmax) == k) x[kk] = y;
-        }
-#endif
-#ifndef SWEEP_FIX_INLOOP
         // the group's pivot rows in this batch (about one batch in five at
         // cfg3, one in sixty at cfg4): their multipliers, in this slot until
         // the next iteration's copies, set aside in fixm -- one wave per row,
@@ -2501,7 +2176,6 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
                 ovf |= __ballot((int)(unsigned)mysr == row);
             }
         }
-#endif
         {
             // write-through stores (SA), as the DPP sweeps'.  A wave whose 64
             // columns lie past the pitch (ld is a multiple of 64, so a wave is
@@ -2518,10 +2192,6 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         }
         slot = slot + 1 == D ? 0 : slot + 1;
     }
-#ifdef SWEEP_PROBE_NO_EPI
-    if (nd > 0) return;                          // timing probe only: results NOT kept
-#endif
-#ifndef SWEEP_FIX_INLOOP
     // the group's pivot rows in this run, rewritten from registers and LDS
     // (pivot row s0: P[s0], then the pivots after s0 -- upd()): every store
     // of the pass has landed and every wave's fixm copies are in
@@ -2531,29 +2201,26 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     for (int f = 0; f < nf; ++f) {
         int meta;
         double mk[NK];
-        if constexpr (SWEEP_FIXLD) {
-            // plain LDS reads (the pass's copies have all landed: vmcnt(0)
-            // above): the row's meta word and its 4 multiplier registers in
-            // one round trip, not five
-            meta = __builtin_amdgcn_readfirstlane(fmeta[f]);
+        // plain LDS reads (the pass's copies have all landed: vmcnt(0)
+        // above): the row's meta word and its 4 multiplier registers in one
+        // round trip, not five
+        meta = __builtin_amdgcn_readfirstlane(fmeta[f]);
 #pragma unroll
-            for (int k = 0; k < NK; ++k) mk[k] = fixm[f][16 * k + (lane & 15)];
-        } else {
-            asm volatile("ds_read_b32 %0, %1\n s_waitcnt lgkmcnt(0)" : "=v"(meta) : "v"(lds_off(&fmeta[f])) : "memory");
-            meta = __builtin_amdgcn_readfirstlane(meta);
-#pragma unroll
-            for (int k = 0; k < NK; ++k) mk[k] = lds_ld64(lds_off(&fixm[f][16 * k + (lane & 15)]));
-        }
+        for (int k = 0; k < NK; ++k) mk[k] = fixm[f][16 * k + (lane & 15)];
         const int s0 = meta & 255;
         double y = pick_p<0, NB, NB>(p, s0);
         fix_chain_dpp<NB>(y, mk, p, s0);
         if (cok) Tout[(r0 + (meta >> 8)) * ld + col] = y;
     }
     if (ovf) fix_rows<NB>(P, M, Tout, ld, col, cok, p, mysr, r0, r1, 0, 0, ovf);
-#endif
-#ifdef SWEEP_PROBE_NO_TAIL
-    if (nd > 0) return;                          // timing probe only: results NOT kept
-#endif
+    if (clk && blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long c1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+        unsigned long long *e = clk + (lseq % SWEEP_CLK_RING) * 4;
+        e[1] = c1 - clk_c0;
+        e[2] = rt1 - clk_r0;
+        e[3] = clk_r0;
+        e[0] = lseq;
+    }
     if (t0 >= t1) return;                        // block-uniform: no tail piece
     // (rows across lanes only where the block's W waves cover its tail in
     // one pass; a longer tail -- tall tableaux on few blocks -- takes the
@@ -2578,7 +2245,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             for (int s = 0; s < NB; ++s) m[s] = M[mq(rr, s)];
             // (no pivot row of the group among the tail's rows -- nearly
             // always -- the chain without the per-pivot row check)
-            const bool tpiv = !SWEEP_TAILQ || __ballot(mysr >= t0 && mysr < t1) != 0;
+            const bool tpiv = __ballot(mysr >= t0 && mysr < t1) != 0;
             for (long long c = tcol; c < tend; ++c) {
                 double x = T[rr * ld + c];
                 const double pv = lane < NB ? P[(long long)lane * ld + c] : 0.0;
@@ -2640,7 +2307,7 @@ __global__ void k_peer_ping(Args A, unsigned tag, unsigned flags, int *ok)
     while (!got) {
         const u64 v = ld_sys(&A.xbuf[p * 8]);
         got = (unsigned)(v >> 32) == tag && ((unsigned)v & 0xffu) == (unsigned)p;
-        f = ((unsigned)v >> 8) & 0xffu;
+        f = ((unsigned)v >> 8) & 0xffffu;
         if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;   // 2 s
         __builtin_amdgcn_s_sleep(2);
     }
@@ -2904,10 +2571,9 @@ static int sweep_blocks_per_cu(const void *fn, int threads)
     return n;
 }
 
-// The sweep launch.  Which kernel (LPGPU_SWEEP_DP=1, the default): k_sweep_rl
-// for groups of 49..64 pivots (the automatic depth of cfg3 and cfg4 is 64, so
-// it is the bench's kernel), k_sweep_dp2 for 17..48 (and the per-pivot
-// path's 32); k_sweep_dp / k_sweep_st stay as A/B variants.  All stores are
+// The sweep launch: k_sweep_rl for groups of 49..64 pivots (the automatic
+// depth of cfg3 and cfg4 is 64, so it is the bench's kernel), k_sweep_dp2 for
+// up to 48 (and every tableau narrower than two 64-column strips).  Stores are
 // write-through (sc1): the tableau lines leave the L2 as they are written
 // instead of in the writeback at the kernel's end (profiles/r01/README.md).
 hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int cnt, hipEvent_t e0, hipEvent_t e1,
@@ -2917,58 +2583,34 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
     // the kernel's depth: the group's known pivot count when the host knows it
     // (a call's last group, explicit pivots), else the handle's depth
     if (cnt > 0 && cnt < nd_max) nd_max = cnt;
-#ifndef SWEEP_SA
-#define SWEEP_SA 16
-#endif
-    constexpr int W = 8, RW = 4, SA = SWEEP_SA;
-    // LPGPU_SWEEP_DP (A/B): 1 (default) k_sweep_dp2 up to 48 pivots per sweep and
-    // k_sweep_rl at 64 (round 3: cfg4 906-931 against 978-980 us per launch,
-    // cfg3 at 64 140 against 149 us; at 48 equal, at 32 96 against 93), 2
-    // k_sweep_dp2 always, 3 k_sweep_dp always (round 2's default at 64), 0
-    // k_sweep_st, 5 k_sweep_rl always
-    static int dpp = -1;
-    if (dpp < 0) {
-        const char *v = std::getenv("LPGPU_SWEEP_DP");
-        dpp = v ? std::atoi(v) : 1;
-    }
-    const int nbq = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
-    if ((dpp == 5 || (dpp == 1 && nbq == 64)) && A.ld % 64 == 0 && A.ld >= 128) {
+    constexpr int RW = 4, SA = 16;
+    // (tests: LPGPU_SWEEP_TAIL=0 -- the last partial strip as a strip of its
+    // own instead of dealt out to every block; 2 -- k_sweep_dp2's tail at any
+    // run length)
+    static const int tail_env = [] {
+        const char *v = std::getenv("LPGPU_SWEEP_TAIL");
+        return v ? std::atoi(v) : 1;
+    }();
+    const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
+    if (nb == 64 && A.ld % 64 == 0 && A.ld >= 128) {
         // k_sweep_rl: strips of 64 W columns, pivot rows in registers, rows
-        // and multipliers streamed into LDS one batch ahead (D = 2: measured
-        // faster than 3 deep).  W = 8 waves for long runs (cfg4: 904 against
-        // 930 us at W = 4), 4 for short ones (cfg3: 141 against 149 us)
-        constexpr int DL = 2;
-        static int w8_env = -1;
-        if (w8_env < 0) {
-            const char *v = std::getenv("LPGPU_SWEEP_W8");   // A/B: 1 = 8 waves at any height
-            w8_env = v ? std::atoi(v) : 0;
-        }
-        const bool w8 = A.rows >= 16384 || w8_env == 1;
-        const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
-#define RL_FN(WV) (nb == 16 ? (const void *)&k_sweep_rl<WV, 16, DL, SA>   \
-                 : nb == 32 ? (const void *)&k_sweep_rl<WV, 32, DL, SA> \
-                 : nb == 48 ? (const void *)&k_sweep_rl<WV, 48, DL, SA> \
-                            : (const void *)&k_sweep_rl<WV, 64, DL, SA>)
+        // and multipliers streamed into LDS.  W = 8 waves for long runs (cfg4:
+        // 904 against 930 us at W = 4) with four batches in flight (one
+        // 243-VGPR workgroup per CU: 902-918 against 916-959 us at two), 4 for
+        // short ones (cfg3: 141 against 149 us; two in flight)
+        const bool w8 = A.rows >= 16384;
         const int WL = w8 ? 8 : 4;
-        const void *fn = w8 ? RL_FN(8) : RL_FN(4);
-#undef RL_FN
-        // batches in flight at 64 pivots, 8 waves: the 254-VGPR kernel runs one
-        // workgroup per CU, so 4 (three batches ahead: 144 KB of LDS) instead
-        // of 2 (cfg4, same-box A/B: 902-918 against 916-959 us per launch);
-        // LPGPU_SWEEP_D=2/3 for A/B
-        static int dl_env = -1;
-        if (dl_env < 0) {
-            const char *v = std::getenv("LPGPU_SWEEP_D");
-            dl_env = v ? std::atoi(v) : 4;
-        }
-        static int dl4_env = -1;
-        if (dl4_env < 0) {
-            const char *v = std::getenv("LPGPU_SWEEP_D4");   // A/B: the same for 4 waves
-            dl4_env = v ? std::atoi(v) : DL;
-        }
-        if (!w8 && nb == 64 && dl4_env == 3) fn = (const void *)&k_sweep_rl<4, 64, 3, SA>;
-        if (w8 && nb == 64 && dl_env == 3) fn = (const void *)&k_sweep_rl<8, 64, 3, SA>;
-        if (w8 && nb == 64 && dl_env == 4) fn = (const void *)&k_sweep_rl<8, 64, 4, SA>;
+        // out of place into the handle's other buffer when it has one (the
+        // host then takes Tout as the tableau; see Args::dflips), with
+        // non-temporal loads and stores (SA | 2): a tableau that large is far
+        // beyond the Infinity Cache, and the pass then does not evict what the
+        // selection keeps there -- cfg4 sweep 787-806 -> 775-781 us, selection
+        // 7.12-7.15 -> 6.84-6.93 us per pivot (same box); at cfg3 (in place)
+        // they cost the selection its cached tableau (4.50 -> 4.65 us)
+        double *To = (A.Tout && A.Tout != A.T) ? A.Tout : A.T;
+        const bool oop = To != A.T;
+        const void *fn = w8 ? (oop ? (const void *)&k_sweep_rl<8, 64, 4, SA | 2> : (const void *)&k_sweep_rl<8, 64, 4, SA>)
+                            : (oop ? (const void *)&k_sweep_rl<4, 64, 2, SA | 2> : (const void *)&k_sweep_rl<4, 64, 2, SA>);
         // a group of nexp = 49..63 pivots: the pivot rows and multipliers
         // past it zeroed (stale rows of an earlier group otherwise; rows of
         // P and entries of MQ that no selection of this group writes), so
@@ -2984,15 +2626,9 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         const int bpc = sweep_blocks_per_cu(fn, 64 * WL);
         // the columns swept: 0..n (the padding past them is 0 and stays 0).
         // Whole strips of 64 WL columns; a last partial strip of <= 64
-        // columns is dealt out to every block (tail) -- LPGPU_SWEEP_TAIL=0:
-        // a strip of its own
-        static int rl_tail = -1;
-        if (rl_tail < 0) {
-            const char *v = std::getenv("LPGPU_SWEEP_TAIL");
-            rl_tail = v ? std::atoi(v) : 1;
-        }
+        // columns is dealt out to every block (tail)
         const long long ncol = A.n + 1, nfull = ncol / (64 * WL), rest = ncol - nfull * 64 * WL;
-        const bool spread = rl_tail != 0 && nfull >= 1 && rest > 0 && rest <= 64;
+        const bool spread = tail_env != 0 && nfull >= 1 && rest > 0 && rest <= 64;
         const long long nsg = spread ? nfull : (ncol + 64 * WL - 1) / (64 * WL);
         const long long slots = (long long)sweep_grid_cus() * bpc;
         long long nrun = slots / nsg;
@@ -3004,110 +2640,53 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         long long tail = spread ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + 7) / 8 * 8 : 0;
         long long tcol = nfull * 64 * WL;
         const double *T = A.T, *Pp = A.P, *Mp = A.MQ;
-        // out of place into the handle's other buffer when it has one (the
-        // host then takes Tout as the tableau; see Args::dflips)
-        double *To = (A.Tout && A.Tout != A.T) ? A.Tout : A.T;
-        unsigned *dfl = To != A.T ? A.dflips : nullptr;
+        unsigned *dfl = oop ? A.dflips : nullptr;
         unsigned fseq = A.flipseq;
-        // out of place (a tableau far beyond the Infinity Cache): the stores
-        // also non-temporal (SA | 2), so the pass does not evict what the
-        // selection keeps there -- cfg4 sweep 787-806 -> 775-781 us, selection
-        // 7.12-7.15 -> 6.84-6.93 us per pivot (same box); at cfg3 (in place)
-        // they cost the selection its cached tableau (4.50 -> 4.65 us)
-        if (To != A.T) {
-            if (fn == (const void *)&k_sweep_rl<8, 64, 4, SA>) fn = (const void *)&k_sweep_rl<8, 64, 4, SA | 2>;
-            else if (fn == (const void *)&k_sweep_rl<4, 64, DL, SA>) fn = (const void *)&k_sweep_rl<4, 64, DL, SA | 2>;
-        }
         const long long *dRp = A.dR;
         const Ctl *ctlp = A.ctl;
         long long ld = A.ld, rows = A.rows;
         int grpv = grp, nsv = (int)nsg;
         long long tend = ncol;
+        unsigned long long *clk = A.sweep_clk;
+        unsigned lseq = A.sweep_lseq;
         void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &tend, &nexp,
-                        &dfl, &fseq};
+                        &dfl, &fseq, &clk, &lseq};
         const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
-        if (err == hipSuccess && flipped) *flipped = To != A.T;
+        if (err == hipSuccess && flipped) *flipped = oop;
         return err != hipSuccess ? err : hipGetLastError();
     }
+    // k_sweep_dp2 (in place), 10-wave workgroups on 128-column strips
+    constexpr int WV = 10;
     const long long ns = (A.ld + 127) / 128;
-    if (dpp) {
-        const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
-        int wv = W;
-        // LPGPU_SWEEP_NT (A/B, off by default): tableau loads non-temporal (aux
-        // nt), 1 always, 2 when the local tableau is far beyond the 256 MB
-        // Infinity Cache.  cfg4 on one GPU: the sweep 1108-1117 -> 1062-1067 us
-        // per 64-pivot launch, but the next selection's column and row reads
-        // slowed by about as much (13.8-14.1 -> 14.3-14.9 us per pivot): 31.9k
-        // against 32.1k pivots/s, within noise (as at cfg3 in round 1)
-        static int nt_env = -1;
-        if (nt_env < 0) {
-            const char *v = std::getenv("LPGPU_SWEEP_NT");
-            nt_env = v ? std::atoi(v) : 0;
-        }
-        const bool nt = nt_env == 1 || (nt_env == 2 && (double)A.rows * (double)A.ld * 8.0 > 1e9);
-        const void *fn = nb == 16 ? (const void *)&k_sweep_dp<W, 16, SA>
-                       : nb == 32 ? (const void *)&k_sweep_dp<W, 32, SA>
-                       : nb == 48 ? (const void *)&k_sweep_dp<W, 48, SA>
-                       : nt       ? (const void *)&k_sweep_dp<W, 64, SA, 2>
-                                  : (const void *)&k_sweep_dp<W, 64, SA>;
-        if (dpp == 2 || (dpp == 1 && nb <= 48)) {
-            wv = 10;
-            fn = nb == 16 ? (const void *)&k_sweep_dp2<10, 16, SA>
-               : nb == 32 ? (const void *)&k_sweep_dp2<10, 32, SA>
-               : nb == 48 ? (const void *)&k_sweep_dp2<10, 48, SA>
-                          : (const void *)&k_sweep_dp2<10, 64, SA>;
-        }
-        const int bpc = sweep_blocks_per_cu(fn, 64 * wv);
-        // the last strip (column n and the pitch's padding) spread over all
-        // blocks where the runs are long: the grid then fills every resident
-        // slot (cfg4: 7 x 65 = 455 of 512 -> 8 x 64 = 512, sweep 1055-1072 ->
-        // 985-987 us per 64-pivot launch); at cfg3's 516-row runs the extra
-        // short piece (a P restage + one batch) costs more than the slots
-        // give back (112.1 -> 114.3-114.6 us).  LPGPU_SWEEP_TAIL (A/B):
-        // 1 (default) runs of >= 2048 rows, 2 always, 0 never
-        static int tail_env = -1;
-        if (tail_env < 0) {
-            const char *v = std::getenv("LPGPU_SWEEP_TAIL");
-            tail_env = v ? std::atoi(v) : 1;
-        }
-        const long long slots = (long long)sweep_grid_cus() * bpc;
-        const bool tailed = ns >= 2 && (tail_env == 2 || (tail_env == 1 && A.rows * (ns - 1) >= 2048 * slots));
-        const long long nsg = tailed ? ns - 1 : ns;   // strips with blocks of their own
-        long long nrun = slots / nsg;
-        if (nrun < 1) nrun = 1;
-        long long run = (A.rows + nrun - 1) / nrun;
-        run = (run + RW - 1) / RW * RW;
-        nrun = (A.rows + run - 1) / run;
-        const dim3 grid((unsigned)(nrun * nsg));
-        // tail rows per block: a multiple of the batch (the multipliers' 4-row quads)
-        long long tail = tailed ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + RW - 1) / RW * RW : 0;
-        const Args *ap = &A;
-        const double *T = ap->T, *Pp = ap->P, *Mp = ap->MQ;   // the sweep reads the quad copy
-        double *To = ap->T;
-        const long long *dRp = ap->dR;
-        const Ctl *ctlp = ap->ctl;
-        long long ld = ap->ld, rows = ap->rows;
-        int grpv = grp, nsv = (int)nsg;
-        void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail};
-        const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * wv), args, 0, s, e0, e1, 0);
-        return err != hipSuccess ? err : hipGetLastError();
-    }
-    const int bpc = nd_max <= 32 ? 3 : nd_max <= 48 ? 2 : 1;
-    long long nrun = (long long)sweep_grid_cus() * bpc / ns;
+    const void *fn = nb == 16 ? (const void *)&k_sweep_dp2<WV, 16, SA>
+                   : nb == 32 ? (const void *)&k_sweep_dp2<WV, 32, SA>
+                   : nb == 48 ? (const void *)&k_sweep_dp2<WV, 48, SA>
+                              : (const void *)&k_sweep_dp2<WV, 64, SA>;
+    const int bpc = sweep_blocks_per_cu(fn, 64 * WV);
+    // the last strip (column n and the pitch's padding) spread over all
+    // blocks where the runs are long (>= 2048 rows per block: the grid then
+    // fills every resident slot); at short runs the extra piece (a P restage
+    // + one batch) costs more than the slots give back
+    const long long slots = (long long)sweep_grid_cus() * bpc;
+    const bool tailed = ns >= 2 && (tail_env == 2 || (tail_env == 1 && A.rows * (ns - 1) >= 2048 * slots));
+    const long long nsg = tailed ? ns - 1 : ns;   // strips with blocks of their own
+    long long nrun = slots / nsg;
     if (nrun < 1) nrun = 1;
     long long run = (A.rows + nrun - 1) / nrun;
     run = (run + RW - 1) / RW * RW;
     nrun = (A.rows + run - 1) / run;
-    const dim3 grid((unsigned)(nrun * ns));
-#define SWEEP_ST_ONE(NBV)                                                                            \
-    hipExtLaunchKernelGGL((k_sweep_st<W, RW, NBV, 0, SA>), grid, dim3(64 * W), 0, s, e0, e1, 0, A.T, A.T, \
-                          A.P, A.MQ, A.dR, A.ctl, A.ld, A.rows, grp, (int)ns, run)
-    if (nd_max <= 16) SWEEP_ST_ONE(16);
-    else if (nd_max <= 32) SWEEP_ST_ONE(32);
-    else if (nd_max <= 48) SWEEP_ST_ONE(48);
-    else SWEEP_ST_ONE(64);
-#undef SWEEP_ST_ONE
-    return hipGetLastError();
+    const dim3 grid((unsigned)(nrun * nsg));
+    // tail rows per block: a multiple of the batch (the multipliers' 4-row quads)
+    long long tail = tailed ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + RW - 1) / RW * RW : 0;
+    const double *T = A.T, *Pp = A.P, *Mp = A.MQ;   // the sweep reads the quad copy
+    double *To = A.T;
+    const long long *dRp = A.dR;
+    const Ctl *ctlp = A.ctl;
+    long long ld = A.ld, rows = A.rows;
+    int grpv = grp, nsv = (int)nsg;
+    void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail};
+    const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WV), args, 0, s, e0, e1, 0);
+    return err != hipSuccess ? err : hipGetLastError();
 }
 
 // ---- k_group geometry and launch ------------------------------------------
@@ -3332,7 +2911,7 @@ hipError_t launch_resume(hipStream_t s, const Args &A)
 
 hipError_t launch_peer_ping(hipStream_t s, const Args &A, unsigned tag, unsigned flags, int *ok_dev)
 {
-    if (A.nranks > NRANK_MAX || !A.xbuf || !A.peer || flags > 0xffu) return hipErrorInvalidValue;
+    if (A.nranks > NRANK_MAX || !A.xbuf || !A.peer || flags > 0xffffu) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_peer_ping, dim3(1), dim3(64), 0, s, A, tag, flags, ok_dev);
     return hipGetLastError();
 }

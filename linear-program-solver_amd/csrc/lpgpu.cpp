@@ -46,6 +46,8 @@ struct lp_handle {
     double *Tb[2] = {nullptr, nullptr};
     unsigned *dflips = nullptr;
     unsigned flips = 0, hflips = 0;
+    unsigned long long *sweep_clk = nullptr;   // lpk::SWEEP_CLK_RING x 4 (Args::sweep_clk)
+    unsigned sweep_lseq = 0;                // k_sweep_rl launches so far
     bool oop = false;
     long long *dR = nullptr, *dC = nullptr;
     lpk::ERec *erec = nullptr;
@@ -68,6 +70,7 @@ struct lp_handle {
     unsigned long long **dpeer = nullptr;   // device table: every rank's buffer
     std::vector<void *> ipc_open;           // peer buffers opened from IPC handles
     bool peer_ok = false;                   // the exchange is set up and validated
+    bool xbuf_fine = false;                 // the exchange buffer is fine-grained device memory
     bool xr_xcd = false;                    // every rank on its own GPU: one-XCD selection
     int xtarget = -1;                       // k_sel's XCD when ranks share a GPU (Args::xtarget)
     int share = 1;                          // most ranks of the job on one GPU (from the ping)
@@ -301,6 +304,8 @@ static Args args_of(const lp_handle *h)
     A.Tout = h->oop ? h->Tb[(h->flips + 1) & 1] : h->T;
     A.dflips = h->dflips;
     A.flipseq = h->flips + 1;
+    A.sweep_clk = h->sweep_clk;
+    A.sweep_lseq = h->sweep_lseq;
     A.row0 = h->row0;
     A.col0 = h->col0;
     A.M = h->M;
@@ -453,26 +458,42 @@ static int alloc_handle(lp_handle *h)
         // by size, only where the second buffer fits with room to spare (the
         // group data below, other handles): a tableau of more than about half
         // the device stays in place rather than failing to open
+        // (test knobs, tests/test_gpu_r6.py: LPGPU_OOP_ROOM_MB, the headroom
+        // asked for beyond the second buffer, default 1 GiB; LPGPU_OOP_FAIL_ALLOC=1
+        // fails the second buffer's allocation as a full device would)
+        static const unsigned long long room_mb = [] {
+            const char *v = std::getenv("LPGPU_OOP_ROOM_MB");
+            return v ? std::strtoull(v, nullptr, 10) : 1024ull;
+        }();
         if (h->oop && oop_env == 2) {
             size_t fr = 0, tot = 0;
             if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
                 (void)hipGetLastError();
                 h->oop = false;
-            } else if (fr < tbytes + tbytes / 8 + ((size_t)1 << 30)) {
+            } else if ((unsigned long long)fr < tbytes + tbytes / 8 + (room_mb << 20)) {
                 h->oop = false;
             }
         }
     }
+    static const bool fail_alloc = [] {
+        const char *v = std::getenv("LPGPU_OOP_FAIL_ALLOC");
+        return v && v[0] == '1';
+    }();
     if (h->oop) {
         // the second buffer: its padding columns stay 0 like T's (no sweep
         // writes past column n).  Unforced, a failed allocation falls back to
         // in-place sweeps.
-        if (hipMalloc(&h->Tb[1], tbytes) != hipSuccess) {
+        if (fail_alloc || hipMalloc(&h->Tb[1], tbytes) != hipSuccess) {
             (void)hipGetLastError();
             h->Tb[1] = nullptr;
             if (oop_env == 1) HCHK(h, hipErrorOutOfMemory);
             h->oop = false;
         }
+    }
+    {
+        const size_t cb = (size_t)lpk::SWEEP_CLK_RING * 4 * sizeof(unsigned long long);
+        HCHK(h, hipMalloc(&h->sweep_clk, cb));
+        HCHK(h, hipMemsetAsync(h->sweep_clk, 0xff, cb, h->s));
     }
     if (h->oop) {
         HCHK(h, hipMemsetAsync(h->Tb[1], 0, tbytes, h->s));
@@ -684,13 +705,18 @@ extern "C" int lp_peer_handle(lp_handle *h, void *ipc64)
     hipIpcMemHandle_t hd;
     if (!h->xbuf) {
         // fine-grained: peers' system-scope stores are visible to this device's
-        // polling loads; plain device memory if that cannot be shared
+        // polling loads.  Plain device memory if that cannot be shared -- usable
+        // only by ranks on this same GPU: lp_peer_open refuses the exchange
+        // when such a buffer would be polled across devices, and
+        // the job keeps its RCCL per-pivot path
+        h->xbuf_fine = true;
         if (hipExtMallocWithFlags((void **)&h->xbuf, xbytes, hipDeviceMallocFinegrained) != hipSuccess ||
             hipIpcGetMemHandle(&hd, h->xbuf) != hipSuccess) {
             if (h->xbuf) (void)hipFree(h->xbuf);
             h->xbuf = nullptr;
             (void)hipGetLastError();
             HCHK(h, hipMalloc(&h->xbuf, xbytes));
+            h->xbuf_fine = false;
         }
         HCHK(h, hipMemset(h->xbuf, 0, xbytes));
     }
@@ -733,7 +759,8 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     // the ping also carries, one-hot, how many ranks share this rank's GPU:
     // the OR over the ranks gives every rank the same maximum (their
     // persistent selections must then all be resident on that GPU at once)
-    const unsigned flag = 1u << (std::min(here, 8) - 1);
+    // (bit 8: this rank's exchange buffer is plain, coarse-grained memory)
+    const unsigned flag = (1u << (std::min(here, 8) - 1)) | (h->xbuf_fine ? 0u : 0x100u);
     const hipError_t e = lpk::launch_peer_ping(h->s, A, 7u, flag, dok);
     if (e == hipSuccess) (void)hipMemcpyAsync(&ok, dok, sizeof(int), hipMemcpyDeviceToHost, h->s);
     const hipError_t e2 = hipStreamSynchronize(h->s);
@@ -748,6 +775,12 @@ extern "C" int lp_peer_open(lp_handle *h, const void *handles)
     const unsigned bits = ((unsigned)ok >> 1) & 0xffu;
     h->share = 1;
     while (h->share < 8 && (bits >> h->share)) ++h->share;
+    // a coarse-grained exchange buffer anywhere, with the ranks on more than
+    // one GPU: polling loads of one device are not guaranteed to see another
+    // device's stores into such memory, so no rank takes the device-side
+    // exchange (every rank sees the same OR of the flags: a collective answer)
+    if ((((unsigned)ok >> 1) & 0x100u) && h->share < h->nranks)
+        return fail(h, LP_DEVICE_ERROR, "exchange buffer not fine-grained across devices");
     h->xr_xcd = h->share == 1;
     h->xtarget = -1;
     if (const char *v = std::getenv("LPGPU_XR_XCD")) {
@@ -808,6 +841,7 @@ extern "C" int lp_destroy(lp_handle *h)
     if (h->Tb[0]) (void)hipFree(h->Tb[0]);
     if (h->Tb[1]) (void)hipFree(h->Tb[1]);
     if (h->dflips) (void)hipFree(h->dflips);
+    if (h->sweep_clk) (void)hipFree(h->sweep_clk);
     if (h->P) (void)hipFree(h->P);
     if (h->M) (void)hipFree(h->M);
     if (h->MQ) (void)hipFree(h->MQ);
@@ -974,6 +1008,7 @@ static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, int cnt, boo
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 0));
     HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), cnt, e0, e1, flipped));
+    ++h->sweep_lseq;
     return LP_PIVOTED;
 }
 
@@ -1823,6 +1858,38 @@ extern "C" int lpdiag_geometry(lp_handle *h, long long *out)
     out[6] = g.sel;
     out[7] = h->hctl->sel_flags;
     out[8] = g.xs;
+    return LP_PIVOTED;
+}
+
+// diagnostics: the per-launch clock records of the 64-pivot sweep (Args::
+// sweep_clk): up to `cap` of the latest, oldest first, 4 values each (launch
+// number, shader cycles, 100 MHz ticks, start tick) -> *n records
+extern "C" int lpdiag_sweep_clocks(lp_handle *h, unsigned long long *out, int cap, int *n)
+{
+    if (!h || !out || !n || cap < 0) return LP_BAD_ARG;
+    HCHK(h, hipSetDevice(h->dev));
+    HCHK(h, hipStreamSynchronize(h->s));
+    std::vector<unsigned long long> ring((size_t)lpk::SWEEP_CLK_RING * 4);
+    HCHK(h, hipMemcpy(ring.data(), h->sweep_clk, ring.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    const long long last = (long long)h->sweep_lseq;
+    const long long first = std::max(0LL, last - std::min<long long>(cap, lpk::SWEEP_CLK_RING));
+    int k = 0;
+    for (long long q = first; q < last; ++q) {
+        const unsigned long long *e = &ring[(size_t)(q % lpk::SWEEP_CLK_RING) * 4];
+        if (e[0] != (unsigned long long)(unsigned)q) continue;   // a launch that returned early (no record)
+        for (int j = 0; j < 4; ++j) out[4 * k + j] = e[j];
+        ++k;
+    }
+    *n = k;
+    return LP_PIVOTED;
+}
+
+// diagnostics: the tableau buffers the sweeps use -- 2 out of place (the
+// sweep reads one and writes the other), 1 in place
+extern "C" int lpdiag_sweep_buffers(const lp_handle *h, int *nbuf)
+{
+    if (!h || !nbuf) return LP_BAD_ARG;
+    *nbuf = h->oop ? 2 : 1;
     return LP_PIVOTED;
 }
 

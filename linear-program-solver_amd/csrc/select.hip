@@ -243,22 +243,7 @@ __device__ __forceinline__ void row_chain(double (&x)[IPL], const double (&mr)[N
 // immediate offset (the per-granule addresses of the general layout, kept
 // live across the pivot loop, cost k_sel about 70 VGPRs).
 constexpr int SEL_SLOT = 64;
-#ifndef SEL_XS_ROWPF
-#define SEL_XS_ROWPF 1         // XS: the shard's candidate row loaded during the cross-shard exchange
-#endif
-#ifndef SEL_PIPE
-#define SEL_PIPE 0             // exchanges keep two polls in flight
-#endif
-#ifndef SEL_W2_DEFAULT
-#define SEL_W2_DEFAULT 0       // the 128-block one-column-per-lane form by default (sel_geom): off,
-                               // 4.89 against 4.33 us per pivot at cfg3 (round 5 A/B)
-#endif
-#ifndef SEL_POLL1
-#define SEL_POLL1 0            // exchanges poll one word of each summary until it arrives
-#endif
-#ifndef SEL_SLEEP
-#define SEL_SLEEP 1            // s_sleep between the polls of an exchange (64 clocks per unit)
-#endif
+constexpr int SEL_SLEEP = 1;   // s_sleep between the polls of an exchange (64 clocks per unit; 0 and 2: no change)
 // a loop-invariant operand moved into a VGPR (the asm makes it look
 // divergent, so it stays there): k_sel keeps most of its kernel arguments,
 // per-block constants and tolerances in VGPRs -- in SGPRs the compiler ran
@@ -340,44 +325,6 @@ __device__ __forceinline__ double dppd(double v)
 // wave minimum (all 64 lanes active), wave-uniform: two quad permutes and two
 // row rotates reduce each row of 16, two row broadcasts fold the rows into
 // lane 63 (the other lanes end with partial or undefined values)
-#ifndef SEL_WMIN_U32
-#define SEL_WMIN_U32 0
-#endif
-#if SEL_WMIN_U32
-// the same minimum over 32-bit order keys (a double's bits with the sign
-// folded so that unsigned order is numeric order): the high words first, then
-// the low words of the lanes that hold the high minimum; each step is ONE
-// v_min_u32 with its DPP operand (the f64 form needs two 32-bit DPP moves and
-// a v_min_f64 per step).  -0.0 orders below +0.0 here; every use of the
-// result only compares it, where the two are equal.
-__device__ __forceinline__ unsigned wumin63(unsigned x)
-{
-    asm("s_nop 1\n"
-        "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
-        "s_nop 1\n"
-        "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
-        "s_nop 1\n"
-        "v_min_u32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf\n"
-        "s_nop 1\n"
-        "v_min_u32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf\n"
-        "s_nop 1\n"
-        "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "s_nop 1\n"
-        "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "s_nop 1\n"
-        : "+v"(x));
-    return __builtin_amdgcn_readlane(x, 63);
-}
-__device__ __forceinline__ double wmin(double v)
-{
-    const unsigned hi = hi32(v), lo = lo32(v), sg = (unsigned)((int)hi >> 31);
-    const unsigned hk = hi ^ (sg | 0x80000000u);
-    const unsigned hm = wumin63(hk);
-    const unsigned lm = wumin63(hk == hm ? lo ^ sg : 0xffffffffu);
-    const unsigned nn = (unsigned)((int)hm >> 31);          // all ones: the minimum is >= +0
-    return mk_d(lm ^ ~nn, hm ^ (nn ? 0x80000000u : 0xffffffffu));
-}
-#else
 __device__ __forceinline__ double wmin(double v)
 {
     v = vmin(v, dppd<0xB1, 0xf>(v));
@@ -388,7 +335,6 @@ __device__ __forceinline__ double wmin(double v)
     v = vmin(v, dppd<0x143, 0xc>(v));
     return rl_d(lo32(v), hi32(v), 63);
 }
-#endif
 // lane l's word of a summary assembled from wave-uniform values: v_writelane
 // per word (a select chain on the lane index compiled to a branch per word)
 template <int L>
@@ -404,26 +350,6 @@ template <bool FAST, int SLOT = SEL_SLOT>
 __device__ __forceinline__ void sel_put(u64 *region, unsigned b, unsigned tag, unsigned w, int n)
 {
     if ((int)threadIdx.x < n) stx<FAST>(&region[threadIdx.x * SLOT + b], ((u64)tag << 32) | w);
-}
-// the per-pivot exchanges' summaries in NR replicas, `stride` granules apart,
-// block b polling replica b % NR: every summary line is then read by 64 / NR
-// blocks per polling round instead of all 64 (the L2 serves one line's
-// requests one after another)
-#ifndef SEL_NREP
-#define SEL_NREP 1
-#endif
-constexpr int SEL_RSTRIDE = 1024;      // ratio summaries: 9 x 64 granules per replica, 2 fit a region
-constexpr int SEL_ESTRIDE = 512;       // row-0 summaries: 8 x 64, 4 fit
-constexpr int SEL_NREP_R = SEL_NREP < 2 ? SEL_NREP : 2;
-constexpr int SEL_NREP_E = SEL_NREP;
-template <bool FAST, int NR>
-__device__ __forceinline__ void sel_put_rep(u64 *region, int stride, unsigned b, unsigned tag, unsigned w, int n)
-{
-    if ((int)threadIdx.x < n) {
-        const u64 v = ((u64)tag << 32) | w;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) stx<FAST>(&region[r * stride + threadIdx.x * SEL_SLOT + b], v);
-    }
 }
 // every block's summary (lane l: block min(l, G - 1)); polls until every
 // granule carries `tag`, bounded by spin_max polls (the host then redoes the
@@ -520,9 +446,6 @@ template <int NG, int STRIDE = SEL_SLOT>
 struct SelPoll {
     const u64 *p;
     u64 v[NG];
-#if SEL_PIPE
-    u64 u[NG];
-#endif
     __device__ __forceinline__ void load(u64 (&d)[NG])
     {
 #pragma unroll
@@ -542,53 +465,12 @@ struct SelPoll {
     {
         p = base + min((unsigned)threadIdx.x, G - 1);
         load(v);
-#if SEL_PIPE
-        load(u);
-#endif
         __builtin_amdgcn_sched_barrier(0);
     }
     __device__ __forceinline__ bool finish(unsigned tag, unsigned (&w)[NG], unsigned *timeout_flag,
                                            unsigned spin_max)
     {
         __builtin_amdgcn_sched_barrier(0);
-#if SEL_PIPE
-        // two polls always in flight: the older one is checked while the
-        // newer one travels, and a new one goes out behind it (unrolled by
-        // two so that no register copy waits for a load in flight)
-        for (unsigned spins = 0;; spins += 2) {
-            if (take(tag, v, w)) return true;
-            load(v);
-            if (take(tag, u, w)) return true;
-            load(u);
-            if (spins > spin_max) {
-                st_sc1(timeout_flag, 1u);
-                return false;
-            }
-        }
-#elif SEL_POLL1
-        // the first load of every summary word is out (issue()); then poll
-        // only the last word of every block until all carry the tag (one
-        // 512-byte load per round instead of NG: the 64 pollers' rounds cost
-        // the XCD's L2 a ninth), read the other words once and check them
-        for (unsigned spins = 0;; ++spins) {
-            if (take(tag, v, w)) return true;
-            if (spins > spin_max) {
-                st_sc1(timeout_flag, 1u);
-                return false;
-            }
-            bool last = (unsigned)(v[NG - 1] >> 32) == tag;
-            while (!wall(last)) {
-                if (++spins > spin_max) {
-                    st_sc1(timeout_flag, 1u);
-                    return false;
-                }
-                __builtin_amdgcn_s_sleep(SEL_SLEEP);
-                v[NG - 1] = ld_sc1(p + (NG - 1) * STRIDE);
-                last = (unsigned)(v[NG - 1] >> 32) == tag;
-            }
-            load(v);
-        }
-#else
         for (unsigned spins = 0;; ++spins) {
             if (take(tag, v, w)) return true;
             if (spins > spin_max) {
@@ -598,7 +480,6 @@ struct SelPoll {
             __builtin_amdgcn_s_sleep(SEL_SLEEP);
             load(v);
         }
-#endif
     }
 };
 
@@ -607,14 +488,9 @@ constexpr int SEL_NGE = 8;   // row-0 summary: l (2), q (2), i, fneg, P[t][i] (2
 constexpr int SEL_NGS = 5;   // rescan / straddle answer: i, a (2), b (2)
 constexpr int SEL_NGX = 7;   // XR rank summary: l (2), global row, a (2), b (2)
 // XS: the shards' summaries are written to one replica per reading shard
-// (A/B build -DXS_SINGLE: one copy that all 512 blocks poll)
-#ifdef XS_SINGLE
-constexpr int XS_NREP = 1;
-#define XS_RD(s) 0
-#else
+// (one copy that all 512 blocks poll: cfg4 selection 7.2-7.4 -> 8.1 us per pivot)
 constexpr int XS_NREP = XS_SHARDS;
 #define XS_RD(s) (s)
-#endif
 
 // pivot TQ's deferred register work (sel_body): its multiplier into m<TQ / 16>
 // [TQ % 16] -- every vector takes a select at the index, in place (a branch
@@ -647,19 +523,13 @@ constexpr int XS_NREP = XS_SHARDS;
 // every shard forms the winner's pivot row itself from the shared tableau (the
 // multipliers are stored write-through for that) -- no row travels.
 // first: as k_group's (call start: reset / eager / enter).
-// W2 (one XCD, single device): 128 blocks of one column per lane (the row
-// chain, the division and the row-0 summary per pivot halve), blocks 0..63
-// own the rows as before; the row-0 summaries are 128 (lane l holds blocks l
-// and l + 64), the ratio summaries 64 (the row blocks').
-template <int IPL, int NB, bool XR, bool FAST, bool XS, bool W2 = false>
+template <int IPL, int NB, bool XR, bool FAST, bool XS>
 __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const unsigned G, int grp, int count,
                                          int from_erec, unsigned seq, int first, int fmode, long long fcap,
                                          double *lP, long long npiv, long long nstd, long long stuck, int rule,
                                          const unsigned shard)
 {
     constexpr int CS = NB + 2;             // LDS stride of a column's pivot values (16-B reads, no conflicts)
-    constexpr int NRE = W2 ? 2 : 1;        // row-0 summaries per lane (blocks lane + 64 k)
-    constexpr int SLOTE = W2 ? 128 : SEL_SLOT;   // granules between granule g and g + 1 of the row-0 region
     constexpr int NK = NB / 16;            // broadcast registers
     const int lane = threadIdx.x;
     Ctl *ctl = A.ctl;
@@ -690,9 +560,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
     // block's share of the variable columns 1..n (column 0 is every block's)
     const long long rps = XS ? (A.rc + XS_SHARDS - 1) / XS_SHARDS : A.rc;   // rows of a shard
     const long long rs0 = XS ? (long long)shard * rps : 0;                   // its first (0-based)
-    static_assert(!W2 || (!XR && !XS && IPL == 1), "k_sel<W2>: one XCD, single device, one column per lane");
-    const unsigned GR = W2 ? G / 2 : G;    // blocks that own rows (and publish ratio summaries)
-    const long long rpb = (rps + GR - 1) / GR;
+    const long long rpb = (rps + G - 1) / G;
     const long long lr0 = vgpr(1 + rs0 + (long long)b * rpb),
                     lr1 = vgpr(min(1 + rs0 + min((long long)b * rpb + rpb, rps), A.rows));
     const long long li = lr0 + lane;
@@ -812,26 +680,14 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         if (!from_erec && !enter) {
             C = ld_sc1(&ctl->c) + 1;
         } else {
-            // (W2: two summaries per lane, blocks lane and lane + 64)
-            double el[NRE], eq[NRE];
-            long long ei[NRE], ef[NRE];
-#pragma unroll
-            for (int k = 0; k < NRE; ++k) {
-                el[k] = INFINITY;
-                eq[k] = 0.0;
-                ei[k] = NONE;
-                ef[k] = NONE;
-            }
+            double el[1] = {INFINITY}, eq[1] = {0.0};
+            long long ei[1] = {NONE}, ef[1] = {NONE};
             if (from_erec) {
-#pragma unroll
-                for (int k = 0; k < NRE; ++k) {
-                    const unsigned bk = lane + 64 * k;
-                    if (bk < G) {
-                        el[k] = ld_sc1(&erecv[bk].l);
-                        ei[k] = ld_sc1(&erecv[bk].i);
-                        eq[k] = ld_sc1(&erecv[bk].q);
-                        ef[k] = ld_sc1(&erecv[bk].fneg);
-                    }
+                if ((unsigned)lane < G) {
+                    el[0] = ld_sc1(&erecv[lane].l);
+                    ei[0] = ld_sc1(&erecv[lane].i);
+                    eq[0] = ld_sc1(&erecv[lane].q);
+                    ef[0] = ld_sc1(&erecv[lane].fneg);
                 }
             } else {
                 double vv[IPL], vmn = INFINITY, pz[IPL];
@@ -846,36 +702,25 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 sel_summary<IPL>(vv, pz, vmn, jc0, tol, sel_, sei_, seq_, spc_, sfn_);
                 const unsigned etag = gtag(seq, 0, 0);
                 drain_stores();
-                sel_put<FAST, SLOTE>(grE, b, etag, esum_words(sel_, seq_, sei_, sfn_, spc_), SEL_NGE);
-#pragma unroll
-                for (int k = 0; k < NRE; ++k) {
-                    unsigned w[SEL_NGE];
-                    const unsigned gk = min(64u, G - 64u * k);
-                    if (!sel_gather<SEL_NGE, SLOTE>(grE + 64 * k, gk, etag, w, &ctlv->bar_timeout, spin))
-                        status = LP_DEVICE_ERROR;
-                    if ((unsigned)lane < gk) {
-                        el[k] = mk_d(w[0], w[1]);
-                        eq[k] = mk_d(w[2], w[3]);
-                        ei[k] = un_idx(w[4]);
-                        ef[k] = un_idx(w[5]);
-                    }
+                sel_put<FAST>(grE, b, etag, esum_words(sel_, seq_, sei_, sfn_, spc_), SEL_NGE);
+                unsigned w[SEL_NGE];
+                if (!sel_gather<SEL_NGE>(grE, G, etag, w, &ctlv->bar_timeout, spin)) status = LP_DEVICE_ERROR;
+                if ((unsigned)lane < G) {
+                    el[0] = mk_d(w[0], w[1]);
+                    eq[0] = mk_d(w[2], w[3]);
+                    ei[0] = un_idx(w[4]);
+                    ef[0] = un_idx(w[5]);
                 }
             }
             if (capped) {
                 C = NONE;
             } else if (rule == LP_RULE_MIN_INDEX) {
-                long long e1 = ef[0];
-#pragma unroll
-                for (int k = 1; k < NRE; ++k) e1 = min(e1, ef[k]);
-                C = wave_min_ll(e1);
+                C = wave_min_ll(ef[0]);
             } else {
-                double e1 = el[0];
-#pragma unroll
-                for (int k = 1; k < NRE; ++k) e1 = vmin(e1, el[k]);
-                const double g = wmin(e1);
+                const double g = wmin(el[0]);
                 if (g < -tol.cost) {
                     const double ethr = tie_band(g, tol.cost_tie);
-                    C = combine_loaded<NRE>(el, ei, eq, G, ethr);
+                    C = combine_loaded<1>(el, ei, eq, G, ethr);
                     if (C < 0) {                // rare: rescan that block's slice of row 0
                         const long long k0 = 1 + (-1 - C) * cpb, k1 = min(k0 + cpb, A.n + 1);
                         long long best = NONE;
@@ -937,7 +782,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         long long ib = NONE;
         double ab = 0.0, bb = 0.0, qb = 0.0;
         if (lb < INFINITY) {
-            const u64 mask = bal(qq <= tie_band(lb, tol.ratio_tie));   // (the band is finite)
+            const u64 mask = bal(qq <= tie_band(lb, tol.ratio_tie));   // (the band is at most DBL_MAX)
             const int f = __builtin_ctzll(mask);
             ib = lr0 + f;
             ab = rl_d(lo32(a), hi32(a), f);
@@ -950,9 +795,8 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         // summary (read from pivot t + 1 on); this pivot's multipliers are
         // stored after it and drained with the next one
         drain_stores();
-        // (W2: only the row blocks publish; fault injection (tests): block 1
-        // (0) never publishes)
-        if (b < GR && !(A.fault == t + 1 && b == min(1u, G - 1) && shard == 0)) {
+        // (fault injection (tests): block 1 (0) never publishes)
+        if (!(A.fault == t + 1 && b == min(1u, G - 1) && shard == 0)) {
             unsigned wv = idx32(ib);
             wv = wl(wv, lo32(lb), 0);
             wv = wl(wv, hi32(lb), 1);
@@ -962,7 +806,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             wv = wl(wv, hi32(bb), 6);
             wv = wl(wv, lo32(qb), 7);
             wv = wl(wv, hi32(qb), 8);
-            sel_put_rep<FAST, SEL_NREP_R>(grR, SEL_RSTRIDE, b, gtag(seq, t, 0), wv, SEL_NGR);
+            sel_put<FAST>(grR, b, gtag(seq, t, 0), wv, SEL_NGR);
         }
         SEL_EV(2);
         SEL_CLK(5);
@@ -970,7 +814,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         //      travel) the multiplier into its register and to memory
         unsigned w[SEL_NGR];
         SelPoll<SEL_NGR> pr;
-        pr.issue(grR + (b % SEL_NREP_R) * SEL_RSTRIDE, GR);
+        pr.issue(grR, G);
         apend = a;
         if (b == 0 && lane == 0) {            // read after the launch only (after the publication:
             *gp(&ctlv->c) = C - 1;            // stores pending at a drain delay the summary)
@@ -1046,13 +890,13 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             prow_issue(Rl);
             prow_finish(avv);
         };
-        const double rl = (unsigned)lane < GR ? mk_d(w[0], w[1]) : INFINITY;
+        const double rl = (unsigned)lane < G ? mk_d(w[0], w[1]) : INFINITY;
         const double g = wmin(rl);
         SEL_DONE(g);
         SEL_CLK(20);
         if (g < INFINITY) {
             const double thr = tie_band(g, tol.ratio_tie);
-            const int bs = __builtin_ctzll(bal(rl <= thr));         // (lanes >= G: rl = inf, thr finite)
+            const int bs = __builtin_ctzll(bal(rl <= thr));         // (rl = inf: no candidate, never inside the clamped band)
             // (block bs has a candidate: its minimum is finite)
             const long long Rc = un_idx(rl32(w[2], bs));
             if constexpr (!XS) prow_issue(Rc);
@@ -1121,14 +965,12 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             // brought that row into the Infinity Cache, where the winning
             // shard's own loads make the other shards' reads of ITS row hits)
             long long Rpre = NONE;
-#if SEL_XS_ROWPF
             if constexpr (!XR) {
                 if (R != NONE) {
                     prow_issue(R);
                     Rpre = R;
                 }
             }
-#endif
             unsigned x[SEL_NGX];
             const unsigned long long xw0 = __builtin_amdgcn_s_memrealtime();
             if (!sel_gather<SEL_NGX, XS_SHARDS>(xsl, XS_SHARDS, gtag(seq, t, 2), x, &ctlv->bar_timeout, spin)) {
@@ -1147,7 +989,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             }
             const double thr = tie_band(gg, tol.ratio_tie);
             if (gg < INFINITY) {
-            const int ps = __builtin_ctzll(bal(lp <= thr));         // (lanes >= XS_SHARDS: inf)
+            const int ps = __builtin_ctzll(bal(lp <= thr));         // (lanes >= XS_SHARDS, shards without a candidate: inf)
             double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
             bool okp;
             const double qs = row_ratio(as, bs, tol, okp);
@@ -1283,7 +1125,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
                 break;
             }
             const double thr = tie_band(gg, tol.ratio_tie);
-            const int ps = __builtin_ctzll(bal(lp <= thr));         // (lanes >= N: inf)
+            const int ps = __builtin_ctzll(bal(lp <= thr));         // (lanes >= N, ranks without a candidate: inf)
             double as = rl_d(x[3], x[4], ps), bs = rl_d(x[5], x[6], ps);
             bool okp;
             const double qs = row_ratio(as, bs, tol, okp);
@@ -1411,26 +1253,14 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         SEL_CLK(21);
         const bool more = t + 1 < count;
         const unsigned etag = gtag(seq, t, 1);
-        if constexpr (W2) {
-            if (more) sel_put<FAST, SLOTE>(grE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
-        } else {
-            if (more) sel_put_rep<FAST, SEL_NREP_E>(grE, SEL_ESTRIDE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
-        }
+        if (more) sel_put<FAST>(grE, b, etag, esum_words(el, eq, ei, efn, epc), SEL_NGE);
         SEL_EV(4);
         SEL_CLK(11);
         // ---- while the summaries travel: the pivot-row values into LDS,
         //      column 0 of the own rows (this pivot's multiplier is a), the
         //      pivot row's register state, the stall bookkeeping, records
-        SelPoll<SEL_NGE, SLOTE> pe;
-        SelPoll<SEL_NGE, SLOTE> pe2;             // W2: blocks 64 + lane
-        if constexpr (W2) {
-            if (more) {
-                pe.issue(grE, 64);
-                pe2.issue(grE + 64, G - 64);
-            }
-        } else {
-            if (more) pe.issue(grE + (b % SEL_NREP_E) * SEL_ESTRIDE, G);
-        }
+        SelPoll<SEL_NGE> pe;
+        if (more) pe.issue(grE, G);
 #pragma unroll
         for (int k = 0; k < IPL; ++k) {
             if (cok[k]) lP[kc[k] * CS + t] = pv[k];
@@ -1484,35 +1314,25 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
         }
         // ---- the next pivot's entering column
         SEL_CLK(12);
-        unsigned we[SEL_NGE], we2[SEL_NGE];
+        unsigned we[SEL_NGE];
         if (!pe.finish(etag, we, &ctlv->bar_timeout, spin)) {
             status = LP_DEVICE_ERROR;
             break;
-        }
-        if constexpr (W2) {
-            if (!pe2.finish(etag, we2, &ctlv->bar_timeout, spin)) {
-                status = LP_DEVICE_ERROR;
-                break;
-            }
         }
         SEL_CLK(13);
         SEL_EV(5);
         {
             // the standard rule's minimum first, unconditionally: the loop's
             // bookkeeping below fills its dependency gaps (behind the rule and
-            // stop branches it ran after them).  (W2: lane l holds blocks l
-            // and 64 + l; block order is the columns' order)
-            const bool in = (unsigned)lane < (W2 ? 64u : G);
+            // stop branches it ran after them)
+            const bool in = (unsigned)lane < G;
             const double el2 = in ? mk_d(we[0], we[1]) : INFINITY;
-            double el2b = INFINITY;
-            if constexpr (W2) el2b = (unsigned)lane + 64 < G ? mk_d(we2[0], we2[1]) : INFINITY;
-            const double g2 = wmin(W2 ? vmin(el2, el2b) : el2);
+            const double g2 = wmin(el2);
             SEL_DONE(g2);
             SEL_CLK(18);
             rule = __builtin_amdgcn_readfirstlane(rule);
             stop = __builtin_amdgcn_readfirstlane(stop);
-            long long ef2 = in ? un_idx(we[5]) : NONE;
-            if constexpr (W2) ef2 = min(ef2, (unsigned)lane + 64 < G ? un_idx(we2[5]) : NONE);
+            const long long ef2 = in ? un_idx(we[5]) : NONE;
             const bool capped = cap >= 0 && npiv >= cap;
             long long Cn = NONE;
             int owner = -1;                   // the block that answers (rescan / min-index)
@@ -1525,27 +1345,12 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
             } else {
                 if (g2 < -tol.cost) {
                     ethr = tie_band(g2, tol.cost_tie);
-                    int bs;
-                    double qs, pb;
-                    long long cb;
-                    if constexpr (W2) {
-                        const u64 ma = bal(el2 <= ethr), mb = bal(el2b <= ethr);
-                        const int fa = ma ? __builtin_ctzll(ma) : 0, fb = mb ? __builtin_ctzll(mb) : 0;
-                        const double qa = rl_d(we[2], we[3], fa), qb2 = rl_d(we2[2], we2[3], fb);
-                        const long long ca = un_idx(rl32(we[4], fa)), cb2 = un_idx(rl32(we2[4], fb));
-                        const double pa = rl_d(we[6], we[7], fa), pb2 = rl_d(we2[6], we2[7], fb);
-                        const bool lo = ma != 0;
-                        bs = lo ? fa : 64 + fb;
-                        qs = lo ? qa : qb2;
-                        cb = lo ? ca : cb2;
-                        pb = lo ? pa : pb2;
-                    } else {
-                        bs = __builtin_ctzll(bal(el2 <= ethr));   // (lanes >= G: inf)
-                        // (every readlane at once, then the check)
-                        qs = rl_d(we[2], we[3], bs);
-                        cb = un_idx(rl32(we[4], bs));
-                        pb = rl_d(we[6], we[7], bs);
-                    }
+                    // (lanes >= G: inf, never inside the clamped band)
+                    const int bs = __builtin_ctzll(bal(el2 <= ethr));
+                    // (every readlane at once, then the check)
+                    const double qs = rl_d(we[2], we[3], bs);
+                    const long long cb = un_idx(rl32(we[4], bs));
+                    const double pb = rl_d(we[6], we[7], bs);
                     if (qs <= ethr) {
                         Cn = cb;
                         f0 = qs;
@@ -1652,7 +1457,7 @@ __device__ __forceinline__ void sel_body(const Args &A, const unsigned b, const 
 
 }  // namespace
 
-template <int IPL, int NB, bool XR, bool XS, bool W2 = false>
+template <int IPL, int NB, bool XR, bool XS>
 __global__ void __launch_bounds__(GROUP_THREADS)
 k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int first, int fmode, int frule,
       long long fcap)
@@ -1714,14 +1519,6 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
             return;
         }
         bool same = !((unsigned)lane < G) || wx[0] == me;
-        if (G > 64) {                          // W2: blocks 64 + lane too
-            unsigned wy[1];
-            if (!sel_gather<1>(grX + 64, G - 64, gtag(seq, 0, 7), wy, &ctl->bar_timeout, A.spin_max)) {
-                if (b == 0 && lane == 0) st_sc1(&ctl->status, (int)LP_DEVICE_ERROR);
-                return;
-            }
-            same = same && (!((unsigned)lane + 64 < G) || wy[0] == me);
-        }
         if (!wall(same)) {
             if (b == 0 && lane == 0) {
                 *gp(&ctl->sel_flags) = 8u | 4u;
@@ -1732,17 +1529,15 @@ k_sel(Args A, int gper, int grp, int count, int from_erec, unsigned seq, int fir
     }
     // diagnostics: 1 one XCD, 4 k_sel, 16 XCD shards
     if (b == 0 && lane == 0 && shard == 0) *gp(&ctl->sel_flags) = XS ? (16u | 4u) : (1u | 4u);
-    sel_body<IPL, NB, XR, true, XS, W2>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
+    sel_body<IPL, NB, XR, true, XS>(A, b, G, grp, count, from_erec, seq, first, fmode, fcap, lP, npiv, nstd, stuck,
                                     rule, shard);
 }
 
 // ---- geometry and launch ----------------------------------------------------
 namespace {
 
-const void *sel_kernel(int ipl, int nb, bool xr, bool xs, bool w2 = false)
+const void *sel_kernel(int ipl, int nb, bool xr, bool xs)
 {
-    if (w2) return (ipl == 1 && nb == 64 && !xr && !xs) ? reinterpret_cast<const void *>(&k_sel<1, 64, false, false, true>)
-                                                        : nullptr;
 #define SEL_K(I, N) (xr ? reinterpret_cast<const void *>(&k_sel<I, N, true, false>) \
                         : reinterpret_cast<const void *>(&k_sel<I, N, false, false>))
 #define SEL_XS(I) reinterpret_cast<const void *>(&k_sel<I, 64, false, true>)
@@ -1777,11 +1572,10 @@ int sel_per_cu(const void *fn, size_t lds)
 GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bool xs_ok, int share)
 {
     GroupGeom G;
-    static int on = -1;
-    if (on < 0) {
+    static const int on = [] {
         const char *v = std::getenv("LPGPU_SEL");   // A/B: 0 = k_group only
-        on = v ? std::atoi(v) : 1;
-    }
+        return v ? std::atoi(v) : 1;
+    }();
     if (!on || rc < 1 || n < 1 || bmax < 1 || bmax > BMAX) return G;
     // one XCD, or (too tall for one: more than 64 x 64 rows) XS_SHARDS row
     // shards of rps rows, one per XCD, each shard's blocks over all columns
@@ -1795,14 +1589,7 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
     // the fewest blocks (g) with every lane at most 4 columns, or more where
     // a block's LDS (the pivot values of its columns) leaves too few blocks
     // per CU for g on one XCD
-    // (LPGPU_SEL_GMIN, A/B: at least that many blocks -- fewer columns per
-    // lane, a shorter row chain -- where they fit)
-    static long long gmin_env = -1;
-    if (gmin_env < 0) {
-        const char *v = std::getenv("LPGPU_SEL_GMIN");
-        gmin_env = v ? std::atoll(v) : 0;
-    }
-    const long long g0 = std::max({(rps + 63) / 64, (n + 255) / 256, std::min(gmin_env, 64LL)});
+    const long long g0 = std::max((rps + 63) / 64, (n + 255) / 256);
     const int nb = bmax <= 32 ? 32 : 64;
     long long g = 0, cpb = 0;
     int ipl = 0, per_cu = 0;
@@ -1837,42 +1624,11 @@ GroupGeom sel_geom(long long rc, long long n, int bmax, int xcd_cus, bool xr, bo
     // (2/4-GPU ranks of cfg4: 1024 / 2048 per XCD), the columns are what a
     // lane's chain walks, and two columns per lane beat four: 8192 x 8192
     // 102.9k -> 109.4k, 16384 x 8192 77.7k -> 80.9k pivots/s (round 5,
-    // scripts/geo_probe.py xs; LPGPU_SEL_XS64=0 for the fewest blocks)
-    static int xs64 = -1;
-    if (xs64 < 0) {
-        const char *v = std::getenv("LPGPU_SEL_XS64");
-        xs64 = v ? std::atoi(v) : 1;
-    }
-    if (xs && xs64 && g0 < 64 && fits(64)) g = 64;
+    // scripts/geo_probe.py xs)
+    if (xs && g0 < 64 && fits(64)) g = 64;
     for (long long gc = g0; g == 0 && !bad && gc <= 64; gc = gc < 64 && gc + 8 > 64 ? 64 : gc + 8)
         if (fits(gc)) g = gc;
     if (g == 0) return G;
-    // W2 (one XCD, single device, 64 pivots): twice the blocks at one column
-    // per lane -- half the row chain, division and row-0 summary per pivot --
-    // with the first half of the blocks owning the rows as before
-    // (LPGPU_SEL_W2: 1 on, 0 off)
-    static int w2_env = -1;
-    if (w2_env < 0) {
-        const char *v = std::getenv("LPGPU_SEL_W2");
-        w2_env = v ? std::atoi(v) : SEL_W2_DEFAULT;
-    }
-    if (w2_env == 1 && !xs && !xr && share <= 1 && nb == 64 && g == 64 && (n + 127) / 128 <= 64) {
-        const long long cpb2 = (n + 127) / 128;
-        const size_t lds2 = ((size_t)cpb2 * (nb + 2) + 8) * sizeof(double);
-        const int pc2 = sel_per_cu(sel_kernel(1, 64, false, false, true), lds2);
-        if (pc2 >= 1 && 128 <= (long long)pc2 * xcd_cus) {
-            G.g = 128;
-            G.nr = 2;
-            G.ipl = 1;
-            G.rpl = 1;
-            G.xmode = 1;
-            G.sel = nb;
-            G.xs = 0;
-            G.lds = lds2;
-            G.per_cu = pc2;
-            return G;
-        }
-    }
     G.g = g;
     G.nr = 1;
     G.ipl = ipl;
@@ -1892,10 +1648,9 @@ hipError_t launch_sel(hipStream_t s, const Args &A, const GroupGeom &geo, int gr
     if (geo.g == 0 || geo.sel == 0 || count < 1 || count > geo.sel) return hipErrorInvalidValue;
     if (xr && (A.nranks > NRANK_MAX || !A.xbuf || !A.peer)) return hipErrorInvalidValue;
     if (geo.xs && geo.xs != XS_SHARDS) return hipErrorInvalidValue;
-    const long long rowblocks = geo.nr == 2 ? geo.g / 2 : geo.g;
-    if (A.rc > 64 * rowblocks * (geo.xs ? XS_SHARDS : 1) || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
-    if (geo.nr == 2 && (geo.g != 128 || xr || geo.xs)) return hipErrorInvalidValue;
-    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0, geo.xs > 0, geo.nr == 2);
+    if (A.rc > 64 * geo.g * (geo.xs ? XS_SHARDS : 1) || A.n > 64LL * geo.ipl * geo.g) return hipErrorInvalidValue;
+    if (geo.nr != 1) return hipErrorInvalidValue;
+    const void *fn = sel_kernel(geo.ipl, geo.sel, xr != 0, geo.xs > 0);
     if (!fn) return hipErrorInvalidValue;
     const dim3 grid((unsigned)(geo.g * 8));
     Args a0 = A;

@@ -332,6 +332,23 @@ class Engine:
         d["xcd_shards_engaged"] = bool(d["flags"] & 16)
         return d
 
+    def sweep_buffers(self) -> int:
+        """diagnostics (lpdiag_sweep_buffers): 2 when the sweeps run out of
+        place (a second tableau buffer), 1 in place"""
+        nb = C.c_int(0)
+        self._check(self.lib.lpdiag_sweep_buffers(self.h, C.byref(nb)), self.h)
+        return nb.value
+
+    def sweep_clocks(self, cap: int = 1024) -> np.ndarray:
+        """diagnostics (lpdiag_sweep_clocks): per 64-pivot sweep launch, its
+        block 0's (launch number, shader cycles, 100 MHz ticks, start tick),
+        the latest `cap` launches oldest first -- cycles / (ticks / 1e8) is
+        the shader clock during that launch"""
+        buf = (C.c_ulonglong * (4 * cap))()
+        n = C.c_int(0)
+        self._check(self.lib.lpdiag_sweep_clocks(self.h, buf, C.c_int(cap), C.byref(n)), self.h)
+        return np.array(buf[:4 * n.value], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+
     def set_xcd_shards(self, on: bool):
         """diagnostics / A/B (lpdiag_set_xcd_shards): a tall single-device
         tableau runs k_sel as one row shard per XCD (default) or k_group"""

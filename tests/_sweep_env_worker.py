@@ -1,6 +1,6 @@
 """Child process of test_gpu_r2.py::test_sweep_grid_modes_bit_exact (and
 test_gpu_r5.py's tail test): the sweep's grid switches (LPGPU_SWEEP_TAIL,
-LPGPU_SWEEP_DP, LPGPU_SWEEP_CUS) are read once per process, so each setting
+LPGPU_SWEEP_CUS) are read once per process, so each setting
 runs here, over several shapes (or SWEEP_SHAPES), against the f64 oracle.
 Prints one line per shape and "ALL OK" at the end."""
 import os

@@ -8,6 +8,7 @@ Run from the repo root (needs /root/reference, read-only):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline 10   # r3.json only
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline-prefix 64   # r4.json, checkpointed
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline-prefix 80 --out r5.json
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --headline-prefix 16 --workload cfg4 --out r6.json
 
 It imports the reference, drives its own ``Tableau``/``Simplex`` on inputs
 from this repo's generator (``lpsol_amd.generators``) or on hand-built LPs,
@@ -342,15 +343,44 @@ def headline_main(k: int):
         json.dump({"standard_k": [fx]}, f, separators=(",", ":"))
 
 
-def headline_prefix_main(k: int, out: str = "r4.json"):
+HEADLINE_WORKLOADS = {
+    # bench.py WORKLOADS, by name: (generator spec, fixture name)
+    "cfg3": ({"gen": {"kind": "mixed", "m": 4096, "ns": 4096, "seed": 3}}, "cfg3_mixed_4096x4096_s3_prefix"),
+    "cfg4": ({"gen": {"kind": "tall", "m": 32768, "ns": 8192, "seed": 3}}, "cfg4_tall_32768x8192_s3_prefix"),
+}
+
+
+def interned_rows(T):
+    """exact.from_array with one Fraction object per distinct float value:
+    the generators draw from a few hundred values, and at cfg4 (268 M cells)
+    separate objects would cost ~33 GB before the first pivot.  Fractions are
+    immutable, so sharing them changes nothing the reference computes."""
+    cache = {}
+    out = []
+    for row in T:
+        r = []
+        for x in row.tolist():
+            f = cache.get(x)
+            if f is None:
+                f = cache[x] = Fraction(x)
+            r.append(f)
+        out.append(r)
+    return out
+
+
+def headline_prefix_main(k: int, out: str = "r4.json", workload: str = "cfg3"):
     """tests/golden/r4.json: the same reference walk as ``headline_main`` on
     the cfg3 bench tableau, extended towards one full 64-pivot bench group and
     CHECKPOINTED: after every reference pivot the prefix so far (sequence and
     exact objective ``-_z`` of the reference, ``tableau.py:82-84``) is written
     atomically, so a run stopped after any number of pivots leaves a valid
     fixture.  Several hours on one core (denominators grow with the pivots)."""
-    spec = {"gen": {"kind": "mixed", "m": 4096, "ns": 4096, "seed": 3}}
-    T, rows = source_of(spec)
+    spec, name = HEADLINE_WORKLOADS[workload]
+    g = spec["gen"]
+    T = gen.tableau(g["kind"], g["m"], g["ns"], g["seed"])
+    shape, sha = T.shape, gen.digest(T)
+    rows = interned_rows(T)
+    del T
     t = ref_tableau_from_rows(rows)
     del rows
     log = []
@@ -365,9 +395,9 @@ def headline_prefix_main(k: int, out: str = "r4.json"):
             end = res
         times.append(round(time.time() - t0, 1))
         fx = {
-            "name": "cfg3_mixed_4096x4096_s3_prefix", "mode": "standard_k", "k": len(log),
-            **spec, "m": int(T.shape[0] - 1), "n": int(T.shape[1] - 1),
-            "sha256": gen.digest(T), "seq": [[r, c] for r, c, _ in log], "end": end,
+            "name": name, "mode": "standard_k", "k": len(log), "workload": workload,
+            **spec, "m": int(shape[0] - 1), "n": int(shape[1] - 1),
+            "sha256": sha, "seq": [[r, c] for r, c, _ in log], "end": end,
             "objective": fs(t.getZ()), "objective_float": float(t.getZ()),
             "ref_seconds": times[-1], "ref_seconds_cumulative": times,
         }
@@ -389,12 +419,15 @@ def main():
     ap.add_argument("--headline-prefix", type=int, default=0, metavar="K",
                     help="only tests/golden/r4.json: up to K reference pivots on the cfg3 bench "
                          "tableau, rewritten after every pivot")
+    ap.add_argument("--workload", default="cfg3", choices=sorted(HEADLINE_WORKLOADS),
+                    help="--headline-prefix: the bench workload whose tableau the reference pivots "
+                         "(cfg4: r6.json, 32768 x 8192 G_tall seed 3, ~25 min per reference pivot)")
     ap.add_argument("--out", default="r4.json",
                     help="--headline-prefix: the fixture file under tests/golden/ (r5.json: K = 80, across "
                          "the first sweep boundary)")
     args = ap.parse_args()
     if args.headline_prefix:
-        headline_prefix_main(args.headline_prefix, args.out)
+        headline_prefix_main(args.headline_prefix, args.out, args.workload)
         return
     if args.extra:
         extra_main()

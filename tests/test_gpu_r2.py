@@ -208,8 +208,7 @@ def test_json_device_solve_matches_reference(fx, tmp_path):
 
 
 # ------------------------------------------------- sweep grid switches
-@pytest.mark.parametrize("env", [{"LPGPU_SWEEP_TAIL": "2"}, {"LPGPU_SWEEP_TAIL": "2", "LPGPU_SWEEP_DP": "2"},
-                                 {"LPGPU_SWEEP_TAIL": "0"}], ids=["tail", "tail-dp2", "no-tail"])
+@pytest.mark.parametrize("env", [{"LPGPU_SWEEP_TAIL": "2"}, {"LPGPU_SWEEP_TAIL": "0"}], ids=["tail", "no-tail"])
 def test_sweep_grid_modes_bit_exact(env):
     """the sweep's last strip dealt out to every workgroup (on by default only
     for long runs, cfg4) forced on and off for small shapes, with both sweep

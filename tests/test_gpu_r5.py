@@ -30,26 +30,6 @@ def test_sweep_tail_rows_beyond_one_pass(shapes):
     assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
 
 
-@pytest.mark.parametrize("shapes,solve", [
-    ("mixed,4096,4096,136,64", "0"),             # cfg3 at full size: two groups and a padded one
-    ("mixed,4040,4100,150,64", "0"),             # rows off the 64-row block, 8140 columns
-    ("mixed,4050,4120,130,64,1", "0"),           # the min-index rule
-    ("pos,4050,4100,70,64", "1"),                # a whole solve (35 pivots, optimal) after the run
-])
-def test_sel_w2_bit_exact(shapes, solve):
-    """k_sel's W2 form (LPGPU_SEL_W2=1: 128 blocks of one column per lane,
-    the first 64 owning the rows; two row-0 summaries per lane): the pivot
-    sequence and every bit of the tableau as oracle/lp_f64.c's, the geometry
-    engaged (2 summaries per lane) and no fallback (simplex.py:218-284,
-    tableau.py:295-308).  W2 engages where every block's columns fill the
-    LDS share that caps 128 blocks on one XCD (8065..8192 columns); it is off
-    by default -- 4.89 against 4.33 us per pivot at cfg3 (round 5 A/B)"""
-    worker = os.path.join(os.path.dirname(__file__), "_sweep_env_worker.py")
-    env = dict(os.environ, LPGPU_SEL_W2="1", SWEEP_SHAPES=shapes, EXPECT_NR="2", SOLVE_TOO=solve)
-    run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=280)
-    assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
-
-
 @pytest.mark.parametrize("kind,m,ns,k,blocks,ipl", [
     ("tall", 8192, 8192, 136, 64, 2),     # a 4-GPU rank of cfg4: 1024 rows per XCD shard, 2 columns per lane
     ("tall", 9000, 6000, 100, 64, 2),     # 1125-row shards, 18 rows per block (the last 9)
