@@ -1778,6 +1778,46 @@ __device__ __forceinline__ void lds_mult(double (&m)[NC], unsigned a)
         lds_mult<NC, C + 1>(m, a);
     }
 }
+// m[C0 .. C0 + 7]
+template <int C0, int NC>
+__device__ __forceinline__ void lds_mult8(double (&m)[NC], unsigned a)
+{
+    lds_mult_one<C0>(m[C0], a);
+    lds_mult_one<C0 + 1>(m[C0 + 1], a);
+    lds_mult_one<C0 + 2>(m[C0 + 2], a);
+    lds_mult_one<C0 + 3>(m[C0 + 3], a);
+    lds_mult_one<C0 + 4>(m[C0 + 4], a);
+    lds_mult_one<C0 + 5>(m[C0 + 5], a);
+    lds_mult_one<C0 + 6>(m[C0 + 6], a);
+    lds_mult_one<C0 + 7>(m[C0 + 7], a);
+}
+// pair c of a batch with the reads pipelined (k_sweep_rl, SWEEP_LDSPIPE):
+// the read of m[c + 8] goes out, then the wait for m[c] -- in issue order
+// m[c] is read 8 + c, so 8 reads may still be in flight (fewer over the last
+// 8 pairs: the count field holds at most 15) -- then pair c's 16 FMAs
+// (Q = 4: four pairs per step, rg_quad's one DPP hazard wait per block: the
+// reads of m[c + 8 .. c + 11] out, then the wait for m[c + 3])
+template <int NC, int Q, int C = 0>
+__device__ __forceinline__ void sweep_pairs(double (&x)[8], double (&m)[NC], const double (&p)[2 * NC], unsigned a)
+{
+    if constexpr (C < NC) {
+        if constexpr (C + 8 < NC) lds_mult_one<C + 8>(m[C + 8], a);
+        if constexpr (Q == 4 && C + 9 < NC) lds_mult_one<C + 9>(m[C + 9], a);
+        if constexpr (Q == 4 && C + 10 < NC) lds_mult_one<C + 10>(m[C + 10], a);
+        if constexpr (Q == 4 && C + 11 < NC) lds_mult_one<C + 11>(m[C + 11], a);
+        constexpr int L = C + Q - 1;                  // the last register this step reads
+        constexpr int K = L + 9 <= NC ? 8 : NC - 1 - L;
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(m[L]) : "n"(K) : "memory");
+        if constexpr (Q == 4) {
+            asm volatile("" : "+v"(m[C]), "+v"(m[C + 1]), "+v"(m[C + 2]));
+            rg_quad(x, m[C], m[C + 1], m[C + 2], m[C + 3], &p[2 * C]);
+        } else {
+            rg_pair(x, m[C], p[2 * C], p[2 * C + 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        sweep_pairs<NC, Q, C + Q>(x, m, p, a);
+    }
+}
 
 // pivots 16 K + j0 .. 16 K + j1 - 1 of a pivot-row chain: y <- fma(-m[lane
 // 16 K + j of the 16-lane row], p[16 K + j], y), the multiplier broadcast by
@@ -1925,11 +1965,14 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_RGQ
 #define SWEEP_RGQ 1            // k_sweep_rl, 4 waves: the FMAs in blocks of four pivot pairs (one DPP hazard
 #endif                         // wait each; cfg3 sweep 106.7-107.9 -> 104.1-104.6 us; 8 waves: no gain seen)
+#ifndef SWEEP_LDSPIPE
+#define SWEEP_LDSPIPE 1        // k_sweep_rl: a batch's LDS reads pipelined with its FMAs (sweep_pairs)
+#endif
 #ifndef SWEEP_RGQ_W8
-#define SWEEP_RGQ_W8 0         // ... and for 8 waves (A/B)
+#define SWEEP_RGQ_W8 1         // ... and for 8 waves (with the pipelined LDS reads: cfg4 1721 -> 1631 kcycles per launch)
 #endif
 #ifndef SWEEP_UBASE_W8
-#define SWEEP_UBASE_W8 0       // the same for 8 waves
+#define SWEEP_UBASE_W8 1       // the same for 8 waves (with the pipelined reads: cfg4 1636 -> 1614 kcycles)
 #endif
 template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
@@ -2097,25 +2140,28 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     const int vh = (lane & 15) >> 3, vk = lane & 7;
     int nf = 0;                                  // pivot rows captured (wave-uniform)
     u64 ovf = 0;                                 // pivot lanes past NF captured rows
-#pragma unroll 1
-    for (long long i = 0; i < nbat; ++i) {
-        // batch i's copies are the oldest outstanding but for the D - 2 later
-        // batches' copies and stores issued since (the copies of the last
-        // batches are issued anyway, re-reading the last one)
-        // (the first D - 1 batches: fewer issued since -- the prologue's
-        // copies have no stores between them)
+    // batch j's copies are the oldest outstanding but for the D - 2 later
+    // batches' copies and stores issued since (the copies of the last
+    // batches are issued anyway, re-reading the last one)
+    // (the first D - 1 batches: fewer issued since -- the prologue's
+    // copies have no stores between them)
+    auto wait_copies = [&](long long j) {
         static_assert(D <= 4, "k_sweep_rl: waits written for D <= 4");
-        if (i >= D - 1) {
+        if (j >= D - 1) {
             if constexpr (D == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else if constexpr (D == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + PER) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + 2 * PER) : "memory");
-        } else if (i == 0) {
+        } else if (j == 0) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 2) * 5) : "memory");
-        } else if (i == 1) {
+        } else if (j == 1) {
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D == 3 ? PER : 5 + PER) : "memory");
         } else {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");   // D == 4, i == 2
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");   // D == 4, j == 2
         }
+    };
+#pragma unroll 1
+    for (long long i = 0; i < nbat; ++i) {
+        wait_copies(i);
         __syncthreads();                         // every wave's copies of batch i are in LDS
         issue(min(i + D - 1, nbat - 1), slot == 0 ? D - 1 : slot - 1);   // the slot batch i - 1 used
         const long long rb = r0 + i * RW;
@@ -2123,7 +2169,23 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         double x[RW], m[NC];
         // multiplier of pivot 2c + h, batch row k (past kmax: row kmax's)
         const int kr = min(vk, kmax);
-        if (kmax == RW - 1) {
+        if (SWEEP_LDSPIPE && kmax == RW - 1) {
+            // the batch's LDS reads pipelined with its FMAs: the rows and the
+            // first 8 multiplier registers, then pair c's FMAs issue as soon
+            // as m[c] has landed while m[c + 8]'s read is in flight (all 40
+            // reads up front behind one lgkmcnt(0): the SIMD's two waves idled
+            // through every batch's LDS round trip, the 8 waves of a CU
+            // contending for the LDS right after the barrier)
+            const unsigned xa = lds_off(&xs[slot][wave * RW * 64 + lane]);
+            const unsigned ma = lds_off(&ms[slot][(kr >> 2) * (4 * BMAX + QP) + (kr & 3) + vh * 4]);
+            lds_rows<RW>(x, xa);
+            lds_mult8<0, NC>(m, ma);
+            // (x's reads are older than the multipliers': the first pair's
+            // wait covers them)
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
+                         "+v"(x[7]));
+            sweep_pairs<NC, (SWEEP_RGQ && (W <= 4 || SWEEP_RGQ_W8) && NC % 4 == 0) ? 4 : 1>(x, m, p, ma);
+        } else if (kmax == RW - 1) {
             // the LDS reads in asm: a compiler-visible read of LDS the copies
             // write made it wait for every copy in flight (vmcnt(0)) first;
             // the wait above already covers this batch's
@@ -2145,7 +2207,9 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
 #pragma unroll
             for (int c = 0; c < NC; ++c) m[c] = mrow[(2 * c + vh) * 4];
         }
-        if constexpr (SWEEP_RGQ && (W <= 4 || SWEEP_RGQ_W8) && NC % 4 == 0) {
+        if (SWEEP_LDSPIPE && kmax == RW - 1) {
+            // (the FMAs ran with the reads above)
+        } else if constexpr (SWEEP_RGQ && (W <= 4 || SWEEP_RGQ_W8) && NC % 4 == 0) {
 #pragma unroll
             for (int c = 0; c < NC; c += 4) rg_quad(x, m[c], m[c + 1], m[c + 2], m[c + 3], &p[2 * c]);
         } else {

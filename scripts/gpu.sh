@@ -45,7 +45,9 @@ summ() {   # one line from a bench JSON log
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 s = d.get("selection", {})
+ck = d["roofline"].get("shader_clock") or {}
 print(sys.argv[1], round(d["value"]), "sweep", round(d["roofline"]["avg_launch_us"], 1),
+      "kcyc", round(ck.get("kcycles_mean", 0), 1), "GHz", round(ck.get("ghz_mean", 0), 3),
       "frac", round(d["roofline"]["frac"], 3), "sel", round(s.get("us_per_pivot", 0), 3),
       "fb", d.get("fallbacks"), "cfg3", round(d.get("cfg3", {}).get("value", 0)),
       "cfg3sel", round(d.get("cfg3", {}).get("selection", {}).get("us_per_pivot", 0), 3),
