@@ -398,9 +398,12 @@ def sweep_clock_summary(eng, steps: int) -> dict:
         return {"launches": 0}
     ghz = c[:, 1] / (c[:, 2] / 1e8) / 1e9
     us = c[:, 2] / 100.0
-    return {"launches": int(len(c)), "ghz_mean": float(ghz.mean()), "ghz_min": float(ghz.min()),
-            "ghz_max": float(ghz.max()), "block0_us_mean": float(us.mean()),
-            "kcycles_mean": float(c[:, 1].mean() / 1e3)}
+    out = {"launches": int(len(c)), "ghz_mean": float(ghz.mean()), "ghz_min": float(ghz.min()),
+           "ghz_max": float(ghz.max()), "block0_us_mean": float(us.mean()),
+           "kcycles_mean": float(c[:, 1].mean() / 1e3)}
+    if len(c) <= 64:
+        out["ghz_per_launch"] = [round(float(g), 3) for g in ghz]
+    return out
 
 
 def timed_run(eng, steps: int, warmup: int, block: int, barrier, every: int, heater=None, heat_ms: float = 0.0):
