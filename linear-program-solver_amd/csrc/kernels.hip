@@ -1778,18 +1778,14 @@ __device__ __forceinline__ void lds_mult(double (&m)[NC], unsigned a)
         lds_mult<NC, C + 1>(m, a);
     }
 }
-// m[C0 .. C0 + 7]
-template <int C0, int NC>
-__device__ __forceinline__ void lds_mult8(double (&m)[NC], unsigned a)
+// m[C .. N)
+template <int N, int NC, int C = 0>
+__device__ __forceinline__ void lds_mult_first(double (&m)[NC], unsigned a)
 {
-    lds_mult_one<C0>(m[C0], a);
-    lds_mult_one<C0 + 1>(m[C0 + 1], a);
-    lds_mult_one<C0 + 2>(m[C0 + 2], a);
-    lds_mult_one<C0 + 3>(m[C0 + 3], a);
-    lds_mult_one<C0 + 4>(m[C0 + 4], a);
-    lds_mult_one<C0 + 5>(m[C0 + 5], a);
-    lds_mult_one<C0 + 6>(m[C0 + 6], a);
-    lds_mult_one<C0 + 7>(m[C0 + 7], a);
+    if constexpr (C < N && C < NC) {
+        lds_mult_one<C>(m[C], a);
+        lds_mult_first<N, NC, C + 1>(m, a);
+    }
 }
 // pair c of a batch with the reads pipelined (k_sweep_rl, SWEEP_LDSPIPE):
 // the read of m[c + 8] goes out, then the wait for m[c] -- in issue order
@@ -1797,16 +1793,24 @@ __device__ __forceinline__ void lds_mult8(double (&m)[NC], unsigned a)
 // 8 pairs: the count field holds at most 15) -- then pair c's 16 FMAs
 // (Q = 4: four pairs per step, rg_quad's one DPP hazard wait per block: the
 // reads of m[c + 8 .. c + 11] out, then the wait for m[c + 3])
+// (SWEEP_AHEAD = A registers read ahead: m[0 .. A) before the first pair,
+// m[C + A .. C + A + Q) at step C; in issue order m[j] is read 8 + j, so
+// after step C's reads A of them may still be in flight)
+#ifndef SWEEP_AHEAD
+#define SWEEP_AHEAD 8
+#endif
 template <int NC, int Q, int C = 0>
 __device__ __forceinline__ void sweep_pairs(double (&x)[8], double (&m)[NC], const double (&p)[2 * NC], unsigned a)
 {
+    constexpr int A = SWEEP_AHEAD;
+    static_assert(A % Q == 0 && A <= 15, "sweep_pairs: read-ahead");
     if constexpr (C < NC) {
-        if constexpr (C + 8 < NC) lds_mult_one<C + 8>(m[C + 8], a);
-        if constexpr (Q == 4 && C + 9 < NC) lds_mult_one<C + 9>(m[C + 9], a);
-        if constexpr (Q == 4 && C + 10 < NC) lds_mult_one<C + 10>(m[C + 10], a);
-        if constexpr (Q == 4 && C + 11 < NC) lds_mult_one<C + 11>(m[C + 11], a);
+        if constexpr (C + A < NC) lds_mult_one<C + A>(m[C + A], a);
+        if constexpr (Q == 4 && C + A + 1 < NC) lds_mult_one<C + A + 1>(m[C + A + 1], a);
+        if constexpr (Q == 4 && C + A + 2 < NC) lds_mult_one<C + A + 2>(m[C + A + 2], a);
+        if constexpr (Q == 4 && C + A + 3 < NC) lds_mult_one<C + A + 3>(m[C + A + 3], a);
         constexpr int L = C + Q - 1;                  // the last register this step reads
-        constexpr int K = L + 9 <= NC ? 8 : NC - 1 - L;
+        constexpr int K = L + A + 1 <= NC ? A : NC - 1 - L;
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(m[L]) : "n"(K) : "memory");
         if constexpr (Q == 4) {
             asm volatile("" : "+v"(m[C]), "+v"(m[C + 1]), "+v"(m[C + 2]));
@@ -2179,7 +2183,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             const unsigned xa = lds_off(&xs[slot][wave * RW * 64 + lane]);
             const unsigned ma = lds_off(&ms[slot][(kr >> 2) * (4 * BMAX + QP) + (kr & 3) + vh * 4]);
             lds_rows<RW>(x, xa);
-            lds_mult8<0, NC>(m, ma);
+            lds_mult_first<SWEEP_AHEAD, NC>(m, ma);
             // (x's reads are older than the multipliers': the first pair's
             // wait covers them)
             asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
