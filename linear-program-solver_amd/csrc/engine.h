@@ -189,6 +189,9 @@ struct Args {
     unsigned sweep_lseq;
 };
 constexpr int SWEEP_CLK_RING = 1024;
+// after the ring: per block of the latest launch {lseq, start tick, pass-end
+// tick, shader cycles of the pass} (lpdiag_sweep_block_clocks)
+constexpr int SWEEP_BLK_MAX = 8192;
 
 // exchange buffer layout (granules of 8 bytes), see kernels.hip (XR)
 constexpr int NRANK_MAX = 64;

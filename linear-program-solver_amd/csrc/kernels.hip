@@ -2281,13 +2281,22 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         if (cok) Tout[(r0 + (meta >> 8)) * ld + col] = y;
     }
     if (ovf) fix_rows<NB>(P, M, Tout, ld, col, cok, p, mysr, r0, r1, 0, 0, ovf);
-    if (clk && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (clk && threadIdx.x == 0) {
         const unsigned long long c1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-        unsigned long long *e = clk + (lseq % SWEEP_CLK_RING) * 4;
-        e[1] = c1 - clk_c0;
-        e[2] = rt1 - clk_r0;
-        e[3] = clk_r0;
-        e[0] = lseq;
+        if (blockIdx.x == 0) {
+            unsigned long long *e = clk + (lseq % SWEEP_CLK_RING) * 4;
+            e[1] = c1 - clk_c0;
+            e[2] = rt1 - clk_r0;
+            e[3] = clk_r0;
+            e[0] = lseq;
+        }
+        if (blockIdx.x < SWEEP_BLK_MAX) {         // every block's pass, the latest launch
+            unsigned long long *e = clk + SWEEP_CLK_RING * 4 + blockIdx.x * 4;
+            e[0] = lseq;
+            e[1] = clk_r0;
+            e[2] = rt1;
+            e[3] = c1 - clk_c0;
+        }
     }
     if (t0 >= t1) return;                        // block-uniform: no tail piece
     // (rows across lanes only where the block's W waves cover its tail in
@@ -2666,7 +2675,10 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         // 904 against 930 us at W = 4) with four batches in flight (one
         // 243-VGPR workgroup per CU: 902-918 against 916-959 us at two), 4 for
         // short ones (cfg3: 141 against 149 us; two in flight)
-        const bool w8 = A.rows >= 16384;
+#ifndef SWEEP_W8_ROWS
+#define SWEEP_W8_ROWS 16384
+#endif
+        const bool w8 = A.rows >= SWEEP_W8_ROWS;
         const int WL = w8 ? 8 : 4;
         // out of place into the handle's other buffer when it has one (the
         // host then takes Tout as the tableau; see Args::dflips), with

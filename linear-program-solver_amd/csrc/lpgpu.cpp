@@ -491,7 +491,7 @@ static int alloc_handle(lp_handle *h)
         }
     }
     {
-        const size_t cb = (size_t)lpk::SWEEP_CLK_RING * 4 * sizeof(unsigned long long);
+        const size_t cb = (size_t)(lpk::SWEEP_CLK_RING + lpk::SWEEP_BLK_MAX) * 4 * sizeof(unsigned long long);
         HCHK(h, hipMalloc(&h->sweep_clk, cb));
         HCHK(h, hipMemsetAsync(h->sweep_clk, 0xff, cb, h->s));
     }
@@ -1878,6 +1878,41 @@ extern "C" int lpdiag_sweep_clocks(lp_handle *h, unsigned long long *out, int ca
         const unsigned long long *e = &ring[(size_t)(q % lpk::SWEEP_CLK_RING) * 4];
         if (e[0] != (unsigned long long)(unsigned)q) continue;   // a launch that returned early (no record)
         for (int j = 0; j < 4; ++j) out[4 * k + j] = e[j];
+        ++k;
+    }
+    *n = k;
+    return LP_PIVOTED;
+}
+
+// diagnostics: every block's pass in the latest 64-pivot sweep launch (4
+// values each: block, start tick, pass-end tick, shader cycles; 100 MHz
+// ticks of one device-wide clock) -> *n blocks
+extern "C" int lpdiag_sweep_block_clocks(lp_handle *h, unsigned long long *out, int cap, int *n)
+{
+    if (!h || !out || !n || cap < 0) return LP_BAD_ARG;
+    HCHK(h, hipSetDevice(h->dev));
+    HCHK(h, hipStreamSynchronize(h->s));
+    std::vector<unsigned long long> blk((size_t)lpk::SWEEP_BLK_MAX * 4);
+    HCHK(h, hipMemcpy(blk.data(), h->sweep_clk + (size_t)lpk::SWEEP_CLK_RING * 4, blk.size() * sizeof(unsigned long long),
+                      hipMemcpyDeviceToHost));
+    // the latest launch that ran (later ones of a batch may have returned at
+    // once: the solve had stopped, or nothing was deferred)
+    unsigned long long last = 0;
+    bool any = false;
+    for (int b = 0; b < lpk::SWEEP_BLK_MAX; ++b) {
+        const unsigned long long v = blk[(size_t)b * 4];
+        if (v == ~0ull) continue;
+        if (!any || v > last) last = v;
+        any = true;
+    }
+    int k = 0;
+    for (int b = 0; any && b < lpk::SWEEP_BLK_MAX && k < cap; ++b) {
+        const unsigned long long *e = &blk[(size_t)b * 4];
+        if (e[0] != last) continue;
+        out[4 * k] = (unsigned long long)b;
+        out[4 * k + 1] = e[1];
+        out[4 * k + 2] = e[2];
+        out[4 * k + 3] = e[3];
         ++k;
     }
     *n = k;

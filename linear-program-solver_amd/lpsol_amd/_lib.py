@@ -349,6 +349,15 @@ class Engine:
         self._check(self.lib.lpdiag_sweep_clocks(self.h, buf, C.c_int(cap), C.byref(n)), self.h)
         return np.array(buf[:4 * n.value], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
 
+    def sweep_block_clocks(self, cap: int = 8192) -> np.ndarray:
+        """diagnostics (lpdiag_sweep_block_clocks): every block's pass in the
+        latest 64-pivot sweep launch -- (block, start tick, pass-end tick,
+        shader cycles), 100 MHz ticks"""
+        buf = (C.c_ulonglong * (4 * cap))()
+        n = C.c_int(0)
+        self._check(self.lib.lpdiag_sweep_block_clocks(self.h, buf, C.c_int(cap), C.byref(n)), self.h)
+        return np.array(buf[:4 * n.value], dtype=np.uint64).reshape(-1, 4).astype(np.int64)
+
     def set_xcd_shards(self, on: bool):
         """diagnostics / A/B (lpdiag_set_xcd_shards): a tall single-device
         tableau runs k_sel as one row shard per XCD (default) or k_group"""
