@@ -55,7 +55,7 @@ HBM_PEAK_GBPS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 F64_PEAK_TFLOPS = 78.6      # float64 vector spec (half the guide's 157.3 TF FP32 vector)
 SWEEP_KERNEL = "k_sweep"          # every sweep kernel's name starts so (the traffic stamp names which)
 SEED = 3
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r05", "hbm_traffic.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r06", "hbm_traffic.json")
 
 # name -> (generator kind, m, ns, description)
 WORKLOADS = {
