@@ -1007,7 +1007,11 @@ static int launch_sweep_timed(lp_handle *h, const Args &A, int grp, int cnt, boo
 {
     hipEvent_t e0, e1;
     CALL(prof_slot(h, &e0, &e1, 0));
-    HCHK(h, lpk::launch_sweep(h->s, A, grp, block_of(h), cnt, e0, e1, flipped));
+    // the caller's Args live across a batch of launches: the clock record's
+    // launch number is this launch's own
+    Args a = A;
+    a.sweep_lseq = h->sweep_lseq;
+    HCHK(h, lpk::launch_sweep(h->s, a, grp, block_of(h), cnt, e0, e1, flipped));
     ++h->sweep_lseq;
     return LP_PIVOTED;
 }

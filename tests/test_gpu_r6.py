@@ -71,3 +71,26 @@ def test_ratio_band_overflow_picks_first_candidate(m, first):
     geo = e.geometry()
     assert geo["kernel"] == "k_sel" and (geo["xcd_shards"] == 8) == (m > 4096), geo
     e.close()
+
+
+def test_sweep_clock_records():
+    """the sweep's per-launch and per-block clock records (Args::sweep_clk,
+    lpdiag_sweep_clocks / lpdiag_sweep_block_clocks; bench.py's
+    roofline.shader_clock): one record per 64-pivot sweep launch, in launch
+    order, cycles and 100 MHz ticks giving a plausible shader clock; every
+    block of the latest launch recorded once"""
+    from lpsol_amd import generators as gen
+    T = gen.tableau("mixed", 1500, 1000, 3)
+    e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+    e.upload(T)
+    e.set_block(64)
+    st, done = e.run(_lib.RULE_STANDARD, 3 * 64)
+    assert done == 3 * 64
+    c = e.sweep_clocks()
+    assert len(c) >= 2 and all(c[i + 1, 0] > c[i, 0] for i in range(len(c) - 1))
+    ghz = c[:, 1] / (c[:, 2] / 1e8) / 1e9
+    assert ((ghz > 0.3) & (ghz < 4.0)).all(), ghz
+    b = e.sweep_block_clocks()
+    assert len(b) > 0 and len(set(b[:, 0].tolist())) == len(b)
+    assert (b[:, 2] >= b[:, 1]).all() and (b[:, 3] > 0).all()
+    e.close()
