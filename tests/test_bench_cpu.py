@@ -136,3 +136,43 @@ def test_upload_feeds_the_heater_the_same_rows_locally_numbered():
     assert [p[0] for p in e.puts] == [0] + [1 + a for a in range(a0, a1, 1024)]
     assert [p[0] for p in h.puts] == [0] + [1 + a - a0 for a in range(a0, a1, 1024)]
     assert [p[1:] for p in e.puts] == [p[1:] for p in h.puts]
+
+
+def test_profile_every_for_times_every_long_sweep():
+    """cfg4 on one GPU (a 2.1 GB local tableau): every sweep launch timed
+    (VERDICT r5); cfg3 and the 8-GPU rank: every 4th / 8th; an explicit
+    --profile-every wins"""
+    assert bench.profile_every_for(32769, 8192, 20, 0) == 1
+    assert bench.profile_every_for(4097, 8192, 20, 0) == 4
+    assert bench.profile_every_for(4097, 8192, 64, 0) == 8
+    assert bench.profile_every_for(32769, 8192, 20, 3) == 3
+
+
+class _ClockEngine:
+    """sweep_clocks() as lpdiag_sweep_clocks returns it: (launch, cycles,
+    100 MHz ticks, start tick), oldest first"""
+
+    def __init__(self, rows):
+        self.rows = np.array(rows, dtype=np.int64)
+
+    def sweep_clocks(self, cap):
+        return self.rows[-cap:]
+
+
+def test_sweep_clock_summary_reads_the_clock():
+    # 1.6 M cycles over 80,000 ticks (800 us) = 2.0 GHz; 1.6 M over 72,727 = 2.2 GHz
+    rows = [[0, 1_600_000, 80_000, 0], [1, 1_600_000, 72_727, 90_000], [2, 1_700_000, 85_000, 170_000]]
+    s = bench.sweep_clock_summary(_ClockEngine(rows), 2)
+    assert s["launches"] == 2
+    assert s["ghz_per_launch"] == [2.2, 2.0]
+    assert abs(s["kcycles_mean"] - 1650.0) < 1e-9
+    assert abs(s["block0_us_mean"] - (727.27 + 850.0) / 2) < 1e-9
+    assert abs(s["ghz_min"] - 2.0) < 1e-9 and abs(s["ghz_max"] - 2.2) < 1e-4
+    assert bench.sweep_clock_summary(_ClockEngine(np.zeros((0, 4))), 4) == {"launches": 0}
+
+
+def test_sweep_clock_summary_survives_a_failing_engine():
+    class Bad:
+        def sweep_clocks(self, cap):
+            raise RuntimeError("no clocks")
+    assert bench.sweep_clock_summary(Bad(), 4) == {"error": "no clocks"}
