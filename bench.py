@@ -94,7 +94,7 @@ def workload(name: str, nranks: int, rank: int):
 
 SRC_FILES = [os.path.join(ROOT, "linear-program-solver_amd", "csrc", f)
              for f in ("kernels.hip", "select.hip", "lpgpu.cpp", "engine.h", "device.h", "Makefile")] + [
-    os.path.join(ROOT, "include", "lpgpu.h")]
+    os.path.join(ROOT, "include", "lpgpu.h"), os.path.join(ROOT, "include", "lpgpu_diag.h")]
 
 
 def lib_digest() -> str:

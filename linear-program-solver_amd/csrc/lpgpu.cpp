@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "../../include/lpgpu_diag.h"
 
 using lpk::Args;
 using lpk::Ctl;
@@ -1834,7 +1835,7 @@ extern "C" int lp_update_time(lp_handle *h, double *ms, int64_t *launches)
 // diagnostic (not part of the C-ABI): k_group phase clocks of the last group
 extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
 {
-    if (!h->stamps) return LP_BAD_ARG;
+    if (!h || !out || !h->stamps) return LP_BAD_ARG;
     HCHK(h, hipMemcpy(out, h->stamps + lpk::BMAX * 16,
                       lpk::GROUP_MAXBLOCKS * lpk::BMAX * 4 * sizeof(long long), hipMemcpyDeviceToHost));
     return LP_PIVOTED;
@@ -1850,6 +1851,7 @@ extern "C" int lpdiag_bstamps(lp_handle *h, long long *out)
 // run
 extern "C" int lpdiag_geometry(lp_handle *h, long long *out)
 {
+    if (!h || !out) return LP_BAD_ARG;
     const Members M = members_of(h);
     int xr = 0;
     const lpk::GroupGeom g = persistent_geom(h, M, &xr);
@@ -1945,7 +1947,7 @@ extern "C" int lpdiag_set_xcd_shards(lp_handle *h, int on)
 
 extern "C" int lpdiag_stamps(lp_handle *h, long long *out)
 {
-    if (!h->stamps) return LP_BAD_ARG;
+    if (!h || !out || !h->stamps) return LP_BAD_ARG;
     HCHK(h, hipMemcpy(out, h->stamps, lpk::BMAX * 16 * sizeof(long long), hipMemcpyDeviceToHost));
     return LP_PIVOTED;
 }

@@ -13,12 +13,13 @@ from lpsol_amd import LinProg, Simplex, Tableau, _lib
 from lpsol_amd.tableau import _fmt
 
 HEADER = os.path.join(ROOT, "include", "lpgpu.h")
+DIAG_HEADER = os.path.join(ROOT, "include", "lpgpu_diag.h")
 
 
-def declared_symbols():
-    text = open(HEADER).read()
+def declared_symbols(path=HEADER, prefix="lp_"):
+    text = open(path).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(lp_\w+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(" + prefix + r"\w+)\s*\(", text)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -28,6 +29,27 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
     assert set(names) == set(_lib.EXPORTS), "ctypes prototypes out of sync with the header"
+
+
+def test_library_exports_every_declared_diagnostic():
+    """include/lpgpu_diag.h: every diagnostic the library exports is declared
+    there, and every declared one is exported"""
+    lib = _lib.load()
+    names = declared_symbols(DIAG_HEADER, "lpdiag_")
+    assert len(names) >= 7
+    for name in names:
+        assert hasattr(lib, name), name
+    src = open(os.path.join(ROOT, "linear-program-solver_amd", "csrc", "lpgpu.cpp")).read()
+    assert sorted(set(re.findall(r'extern "C" int (lpdiag_\w+)\(', src))) == names
+    # null handles are refused without touching a device
+    assert lib.lpdiag_geometry(None, None) == _lib.BAD_ARG
+    assert lib.lpdiag_stamps(None, None) == _lib.BAD_ARG
+    assert lib.lpdiag_bstamps(None, None) == _lib.BAD_ARG
+    assert lib.lpdiag_sweep_buffers(None, None) == _lib.BAD_ARG
+    n = ctypes.c_int(0)
+    assert lib.lpdiag_sweep_clocks(None, None, 4, ctypes.byref(n)) == _lib.BAD_ARG
+    assert lib.lpdiag_sweep_block_clocks(None, None, 4, ctypes.byref(n)) == _lib.BAD_ARG
+    assert lib.lpdiag_set_xcd_shards(None, 1) == _lib.BAD_ARG
 
 
 def test_library_is_gfx950_code_object():
