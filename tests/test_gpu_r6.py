@@ -94,3 +94,23 @@ def test_sweep_clock_records():
     assert len(b) > 0 and len(set(b[:, 0].tolist())) == len(b)
     assert (b[:, 2] >= b[:, 1]).all() and (b[:, 3] > 0).all()
     e.close()
+
+
+def test_sweep_clock_ring_wraps():
+    """more sweep launches than the ring holds (SWEEP_CLK_RING = 1024): the
+    latest 1024 records come back, oldest first, in launch order"""
+    from lpsol_amd import generators as gen
+    T = gen.tableau("mixed", 512, 512, 3)
+    e = _lib.Engine(T.shape[0] - 1, T.shape[1] - 1)
+    e.set_block(64)
+    for _ in range(20):                        # 20 x 56 = 1120 sweep launches
+        e.upload(T)
+        st, done = e.run(_lib.RULE_STANDARD, 56 * 64)
+        assert done == 56 * 64, (st, done)
+    c = e.sweep_clocks(4096)
+    assert len(c) == 1024, len(c)
+    assert (np.diff(c[:, 0]) > 0).all()
+    assert c[-1, 0] >= 1100 and c[-1, 0] - c[0, 0] >= 1023
+    ghz = c[:, 1] / (c[:, 2] / 1e8) / 1e9
+    assert ((ghz > 0.3) & (ghz < 4.0)).all()
+    e.close()
