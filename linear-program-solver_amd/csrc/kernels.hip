@@ -1983,7 +1983,7 @@ __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
            const long long *__restrict__ dR, const Ctl *__restrict__ ctl, long long ld, long long rows, int grp,
            int nstrips, long long run, long long tail, long long tcol, long long tend, int nexp,
-           unsigned *dflips, unsigned flipseq, unsigned long long *clk, unsigned lseq)
+           unsigned *dflips, unsigned flipseq, unsigned long long *clk, unsigned lseq, long long runb, int na)
 {
     // tail > 0: the grid covers strips [0, nstrips) of the columns and the 64
     // columns from tcol (the tableau's last columns: n + 1 is rarely a
@@ -2037,8 +2037,12 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     if (threadIdx.x < NB) sr[threadIdx.x] = (int)threadIdx.x < nd ? dR[threadIdx.x] : -2;
     auto srow = [&](int s) -> long long { return sr[s]; };
     const int strip = (int)(blockIdx.x % (unsigned)nstrips);
-    const long long r0 = (long long)(blockIdx.x / (unsigned)nstrips) * run;
-    const long long r1 = min(rows, r0 + run);
+    // row run ri of the strip: runs 0 .. na - 1 of `run` rows, the rest of
+    // runb (two workgroups per CU: the grid's first half, dispatched first,
+    // takes the longer runs -- see launch_sweep)
+    const long long ri = (long long)(blockIdx.x / (unsigned)nstrips);
+    const long long r0 = ri < na ? ri * run : (long long)na * run + (ri - na) * runb;
+    const long long r1 = min(rows, r0 + (ri < na ? run : runb));
     // this lane's column.  Lanes past the pitch (the last strip of a pitch
     // that is not a multiple of 64 W: whole waves) load from column ld - 2 /
     // ld - 1 and their stores are dropped (below), so every wave issues the
@@ -2716,6 +2720,34 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         long long run = (A.rows + nrun - 1) / nrun;
         run = (run + 7) / 8 * 8;                 // whole 8-row batches (the multipliers' quads)
         nrun = (A.rows + run - 1) / run;
+        // Two workgroups per CU (the 4-wave pass): the grid's first half of
+        // runs -- dispatched first, each CU's older workgroup, which the
+        // CU's wave-age issue priority runs ahead -- takes SWEEP_SPLIT of the
+        // rows, the second half the rest.  Equal runs ended bimodally (the
+        // older workgroups at 66-78 us, the younger, then alone on the CU at
+        // one wave per SIMD, at 93-102 us: profiles/r06/sweep_blocks_r06_cfg3.txt);
+        // cfg3 sweep 104-106 -> 98-100 us (profiles/r06/ab_r06_sweep_split.txt).
+        // LPGPU_SWEEP_SPLIT=f overrides (0: equal runs)
+#ifndef SWEEP_SPLIT
+#define SWEEP_SPLIT 0.62
+#endif
+        static const double split_env = [] {
+            const char *v = std::getenv("LPGPU_SWEEP_SPLIT");
+            return v ? std::atof(v) : SWEEP_SPLIT;
+        }();
+        long long runb = run;
+        int na = (int)nrun;
+        if (split_env > 0.0 && split_env < 1.0 && bpc == 2 && nrun >= 2 && nrun % 2 == 0) {
+            const long long h = nrun / 2;
+            long long ra = ((long long)(split_env * (double)A.rows) / h + 7) / 8 * 8;
+            long long rb = ((A.rows - h * ra + h - 1) / h + 7) / 8 * 8;
+            // (every run starts inside the tableau and the runs cover it)
+            if (ra > 0 && rb > 0 && h * ra + h * rb >= A.rows && h * ra + (h - 1) * rb < A.rows) {
+                run = ra;
+                runb = rb;
+                na = (int)h;
+            }
+        }
         const dim3 grid((unsigned)(nrun * nsg));
         long long tail = spread ? ((A.rows + nrun * nsg - 1) / (nrun * nsg) + 7) / 8 * 8 : 0;
         long long tcol = nfull * 64 * WL;
@@ -2730,7 +2762,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         unsigned long long *clk = A.sweep_clk;
         unsigned lseq = A.sweep_lseq;
         void *args[] = {&T, &To, &Pp, &Mp, &dRp, &ctlp, &ld, &rows, &grpv, &nsv, &run, &tail, &tcol, &tend, &nexp,
-                        &dfl, &fseq, &clk, &lseq};
+                        &dfl, &fseq, &clk, &lseq, &runb, &na};
         const hipError_t err = hipExtLaunchKernel(fn, grid, dim3(64 * WL), args, 0, s, e0, e1, 0);
         if (err == hipSuccess && flipped) *flipped = oop;
         return err != hipSuccess ? err : hipGetLastError();

@@ -8,6 +8,9 @@
   tie_band), so lanes and blocks without a candidate (+inf) never pass the
   ballot and the leaving row is the first candidate, as oracle/lp_f64.c's
   +inf band picks it -- on the one-XCD selection and on the XCD shards.
+* The 4-wave sweep's unequal row runs (launch_sweep, SWEEP_SPLIT: each
+  CU's older workgroup takes the longer run): at several splits, equal runs
+  included, on shapes whose runs come out even, against the f64 oracle.
 
 Reference: /root/reference/lpsol/simplex.py:251-284 (findPivotStandard: the
 ratio test's first row with the minimum ratio), tableau.py:269-280 (rowAdd).
@@ -114,3 +117,20 @@ def test_sweep_clock_ring_wraps():
     ghz = c[:, 1] / (c[:, 2] / 1e8) / 1e9
     assert ((ghz > 0.3) & (ghz < 4.0)).all()
     e.close()
+
+
+# (kind, m, ns, pivots, pivots per sweep): 16-32 row runs of two workgroups per
+# CU (nrun even), row counts off the 8-row batch
+SPLIT_SHAPES = "mixed,3001,2100,130,64;pos,2300,1500,70,64;mixed,5003,2100,70,64"
+
+
+@pytest.mark.parametrize("split", ["0", "0.55", "0.7"])
+def test_sweep_run_split_bit_exact(split):
+    """k_sweep_rl with the grid's first half of row runs longer than the
+    second (LPGPU_SWEEP_SPLIT; the default 0.62 runs in every other test):
+    the pivot sequence and every bit of the tableau as oracle/lp_f64.c's
+    (tableau.py:269-280)"""
+    worker = os.path.join(os.path.dirname(__file__), "_sweep_env_worker.py")
+    env = dict(os.environ, LPGPU_SWEEP_SPLIT=split, SWEEP_SHAPES=SPLIT_SHAPES)
+    run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=110)
+    assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
