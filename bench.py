@@ -68,6 +68,10 @@ WORKLOADS = {
     # one such rank's shape alone on one GPU (no cross-rank exchange): the
     # baseline the rehearsal's XR overhead is measured against
     "cfg4r8one": ("tall", 4096, 6144, "4096x6144 G_tall seed 3: one cfg4r8 rank's shape on one GPU"),
+    # one rank's rows of the 4- and 2-GPU cfg4 job alone on one GPU (8192 /
+    # 16384 rows of the 8192-column tableau; no cross-rank exchange)
+    "cfg4r4one": ("tall", 8192, 8192, "8192x8192 G_tall seed 3: one 4-GPU cfg4 rank's rows on one GPU"),
+    "cfg4r2one": ("tall", 16384, 8192, "16384x8192 G_tall seed 3: one 2-GPU cfg4 rank's rows on one GPU"),
 }
 
 

@@ -124,13 +124,13 @@ def test_sweep_clock_ring_wraps():
 SPLIT_SHAPES = "mixed,3001,2100,130,64;pos,2300,1500,70,64;mixed,5003,2100,70,64"
 
 
-@pytest.mark.parametrize("split", ["0", "0.55", "0.7"])
-def test_sweep_run_split_bit_exact(split):
+@pytest.mark.parametrize("split,oop", [("0", "0"), ("0.55", "0"), ("0.7", "0"), ("0.62", "1")])
+def test_sweep_run_split_bit_exact(split, oop):
     """k_sweep_rl with the grid's first half of row runs longer than the
     second (LPGPU_SWEEP_SPLIT; the default 0.62 runs in every other test):
-    the pivot sequence and every bit of the tableau as oracle/lp_f64.c's
-    (tableau.py:269-280)"""
+    the pivot sequence and every bit of the tableau as oracle/lp_f64.c's,
+    in place and out of place (tableau.py:269-280)"""
     worker = os.path.join(os.path.dirname(__file__), "_sweep_env_worker.py")
-    env = dict(os.environ, LPGPU_SWEEP_SPLIT=split, SWEEP_SHAPES=SPLIT_SHAPES)
+    env = dict(os.environ, LPGPU_SWEEP_SPLIT=split, LPGPU_SWEEP_OOP=oop, SWEEP_SHAPES=SPLIT_SHAPES)
     run = subprocess.run([sys.executable, "-u", worker], env=env, capture_output=True, text=True, timeout=110)
     assert run.returncode == 0 and "ALL OK" in run.stdout, run.stdout + run.stderr
