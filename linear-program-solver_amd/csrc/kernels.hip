@@ -1972,12 +1972,6 @@ __device__ __forceinline__ void fix_rows(const double *__restrict__ P, const dou
 #ifndef SWEEP_LDSPIPE
 #define SWEEP_LDSPIPE 1        // k_sweep_rl: a batch's LDS reads pipelined with its FMAs (sweep_pairs)
 #endif
-#ifndef SWEEP_RGQ_W8
-#define SWEEP_RGQ_W8 1         // ... and for 8 waves (with the pipelined LDS reads: cfg4 1721 -> 1631 kcycles per launch)
-#endif
-#ifndef SWEEP_UBASE_W8
-#define SWEEP_UBASE_W8 1       // the same for 8 waves (with the pipelined reads: cfg4 1636 -> 1614 kcycles)
-#endif
 template <int W, int NB, int D, int SA>
 __global__ void __launch_bounds__(64 * W)
 k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const double *__restrict__ M,
@@ -2093,7 +2087,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
     auto issue = [&](long long i, int slot) {
         const long long rb = r0 + i * RW;
         const long long last = r1 - 1;
-        constexpr int UB = W <= 4 ? SWEEP_UBASE : SWEEP_UBASE_W8;
+        constexpr int UB = SWEEP_UBASE;
         if (UB == 1 && rb + RW - 1 <= last) {
             // buffer loads into LDS: the batch's row as the resource base
             // (scalar), the lane's offset a 32-bit VGPR
@@ -2192,7 +2186,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
             // wait covers them)
             asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]),
                          "+v"(x[7]));
-            sweep_pairs<NC, (SWEEP_RGQ && (W <= 4 || SWEEP_RGQ_W8) && NC % 4 == 0) ? 4 : 1>(x, m, p, ma);
+            sweep_pairs<NC, (SWEEP_RGQ && NC % 4 == 0) ? 4 : 1>(x, m, p, ma);
         } else if (kmax == RW - 1) {
             // the LDS reads in asm: a compiler-visible read of LDS the copies
             // write made it wait for every copy in flight (vmcnt(0)) first;
@@ -2217,7 +2211,7 @@ k_sweep_rl(const double *T, double *Tout, const double *__restrict__ P, const do
         }
         if (SWEEP_LDSPIPE && kmax == RW - 1) {
             // (the FMAs ran with the reads above)
-        } else if constexpr (SWEEP_RGQ && (W <= 4 || SWEEP_RGQ_W8) && NC % 4 == 0) {
+        } else if constexpr (SWEEP_RGQ && NC % 4 == 0) {
 #pragma unroll
             for (int c = 0; c < NC; c += 4) rg_quad(x, m[c], m[c + 1], m[c + 2], m[c + 3], &p[2 * c]);
         } else {
@@ -2675,15 +2669,13 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
     const int nb = nd_max <= 16 ? 16 : nd_max <= 32 ? 32 : nd_max <= 48 ? 48 : 64;
     if (nb == 64 && A.ld % 64 == 0 && A.ld >= 128) {
         // k_sweep_rl: strips of 64 W columns, pivot rows in registers, rows
-        // and multipliers streamed into LDS.  W = 8 waves for long runs (cfg4:
-        // 904 against 930 us at W = 4) with four batches in flight (one
-        // 243-VGPR workgroup per CU: 902-918 against 916-959 us at two), 4 for
-        // short ones (cfg3: 141 against 149 us; two in flight)
-#ifndef SWEEP_W8_ROWS
-#define SWEEP_W8_ROWS 16384
-#endif
-        const bool w8 = A.rows >= SWEEP_W8_ROWS;
-        const int WL = w8 ? 8 : 4;
+        // and multipliers streamed into LDS; W = 4 waves, two batches in
+        // flight, two workgroups per CU, row runs split by workgroup age
+        // (below).  (Until late in round 6 runs of 16384+ rows -- cfg4 --
+        // took one 8-wave, 4-deep workgroup per CU; with the split the 4-wave
+        // pass is faster there too: cfg4 785-817 -> 759-779 us per launch on
+        // two boxes, the 16384-row rank equal, profiles/r06/ab_r06_sweep_w4.txt)
+        constexpr int WL = 4;
         // out of place into the handle's other buffer when it has one (the
         // host then takes Tout as the tableau; see Args::dflips), with
         // non-temporal loads and stores (SA | 2): a tableau that large is far
@@ -2693,8 +2685,7 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         // they cost the selection its cached tableau (4.50 -> 4.65 us)
         double *To = (A.Tout && A.Tout != A.T) ? A.Tout : A.T;
         const bool oop = To != A.T;
-        const void *fn = w8 ? (oop ? (const void *)&k_sweep_rl<8, 64, 4, SA | 2> : (const void *)&k_sweep_rl<8, 64, 4, SA>)
-                            : (oop ? (const void *)&k_sweep_rl<4, 64, 2, SA | 2> : (const void *)&k_sweep_rl<4, 64, 2, SA>);
+        const void *fn = oop ? (const void *)&k_sweep_rl<4, 64, 2, SA | 2> : (const void *)&k_sweep_rl<4, 64, 2, SA>;
         // a group of nexp = 49..63 pivots: the pivot rows and multipliers
         // past it zeroed (stale rows of an earlier group otherwise; rows of
         // P and entries of MQ that no selection of this group writes), so

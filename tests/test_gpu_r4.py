@@ -187,8 +187,8 @@ def test_cfg3_reference_prefix_full_group():
 # (kind, m, ns): the k_sweep_rl tail -- the last n + 1 - 64 W floor((n + 1) /
 # 64 W) columns dealt out to every workgroup -- at 1, 2, 4 columns (rows
 # across lanes, one chain per row with the pivot rows' P[s] taken in it) and
-# 5, 33, 64 (columns across lanes); 4-wave (mixed, 1000 rows: 256-column
-# strips) and 8-wave workgroups (tall, 16500 rows: 512-column strips)
+# 5, 33, 64 (columns across lanes); short (mixed, 1000 rows) and long row
+# runs (tall, 16500 rows), 256-column strips
 TAILS = [("mixed", 1000, 24), ("mixed", 1000, 25), ("mixed", 1000, 27), ("mixed", 1000, 28),
          ("mixed", 1000, 56), ("mixed", 1000, 87), ("tall", 16500, 512), ("tall", 16500, 514),
          ("tall", 16500, 551)]
