@@ -168,6 +168,9 @@ struct Args {
     // block 0 lands on); 0..7 the blocks that find themselves on XCD xtarget
     // work -- ranks sharing one GPU each take their own XCD (lpgpu.cpp)
     int xtarget;
+    // ranks of this job sharing this rank's GPU (tests, rehearsals; 1 in a
+    // real multi-GPU job): launch_sweep keeps the 8-wave pass there
+    int share;
     int fault_xcc;       // tests only (LPGPU_FAULT_XCC): block 1 (shard 0) reports another XCD
     // row-sharded persistent selection: this rank's exchange buffer and every
     // rank's (peer[rank] == xbuf), written by the peers over xGMI

@@ -2674,8 +2674,15 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         // (below).  (Until late in round 6 runs of 16384+ rows -- cfg4 --
         // took one 8-wave, 4-deep workgroup per CU; with the split the 4-wave
         // pass is faster there too: cfg4 785-817 -> 759-779 us per launch on
-        // two boxes, the 16384-row rank equal, profiles/r06/ab_r06_sweep_w4.txt)
-        constexpr int WL = 4;
+        // two boxes, the 16384-row rank equal, profiles/r06/ab_r06_sweep_w4.txt).
+        // Ranks sharing one GPU (tests and rehearsals: A.share > 1) with
+        // 16384+ rows keep the 8-wave pass, one workgroup per CU: each rank's
+        // XCD-shard selection is persistent and holds a wave on the CUs'
+        // SIMDs while the other rank still sweeps, and the 4-wave pass's
+        // 512 workgroups could then not all be placed (a co-located 2-GPU
+        // rank pair timed out, tests/test_gpu_r4_procs.py)
+        const bool w8 = A.share > 1 && A.rows >= 16384;
+        const int WL = w8 ? 8 : 4;
         // out of place into the handle's other buffer when it has one (the
         // host then takes Tout as the tableau; see Args::dflips), with
         // non-temporal loads and stores (SA | 2): a tableau that large is far
@@ -2685,7 +2692,8 @@ hipError_t launch_sweep(hipStream_t s, const Args &A, int grp, int nd_max, int c
         // they cost the selection its cached tableau (4.50 -> 4.65 us)
         double *To = (A.Tout && A.Tout != A.T) ? A.Tout : A.T;
         const bool oop = To != A.T;
-        const void *fn = oop ? (const void *)&k_sweep_rl<4, 64, 2, SA | 2> : (const void *)&k_sweep_rl<4, 64, 2, SA>;
+        const void *fn = w8 ? (oop ? (const void *)&k_sweep_rl<8, 64, 4, SA | 2> : (const void *)&k_sweep_rl<8, 64, 4, SA>)
+                            : (oop ? (const void *)&k_sweep_rl<4, 64, 2, SA | 2> : (const void *)&k_sweep_rl<4, 64, 2, SA>);
         // a group of nexp = 49..63 pivots: the pivot rows and multipliers
         // past it zeroed (stale rows of an earlier group otherwise; rows of
         // P and entries of MQ that no selection of this group writes), so

@@ -347,6 +347,7 @@ static Args args_of(const lp_handle *h)
     A.hier = hier;
     A.rank = h->rank;
     A.xtarget = h->xtarget;
+    A.share = h->share;
     A.fault_xcc = 0;
     A.xbuf = h->xbuf;
     A.peer = h->dpeer;
