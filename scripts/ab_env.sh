@@ -14,6 +14,7 @@ for i in $(seq 1 "$n"); do
     if [ $rc -ne 0 ]; then echo "$wl [$setting] rc=$rc" | tee -a gpurun_out/ab.txt; tail -3 gpurun_out/ab.err; exit $rc; fi
     python -c "
 import json; d=json.loads(open('gpurun_out/ab.json').read().strip().splitlines()[-1])
-print('$wl', '[$setting]', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'],1), 'frac', round(d['roofline']['frac'],3), 'sel', round(d['selection']['us_per_pivot'],2), 'fb', d['fallbacks'])" | tee -a gpurun_out/ab.txt
+ck=d['roofline'].get('shader_clock') or {}
+print('$wl', '[$setting]', round(d['value']), 'sweep', round(d['roofline']['avg_launch_us'],1), 'kcyc', round(ck.get('kcycles_mean',0),1), 'GHz', round(ck.get('ghz_mean',0),3), 'frac', round(d['roofline']['frac'],3), 'sel', round(d['selection']['us_per_pivot'],2), 'fb', d['fallbacks'])" | tee -a gpurun_out/ab.txt
   done
 done
